@@ -1,0 +1,31 @@
+#!/usr/bin/env bash
+# Builds hcunet_amd/libhcunet.so for gfx950 (hipcc cross-compiles without a GPU).
+# Usage: ./build.sh [extra hipcc flags]
+set -euo pipefail
+cd "$(dirname "$0")"
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+OUT=hcunet_amd/libhcunet.so
+SRC="hcunet_amd/csrc/gconv.hip hcunet_amd/csrc/wgrad.hip hcunet_amd/csrc/pointwise.hip hcunet_amd/csrc/loss_adam.hip hcunet_amd/csrc/unet.cpp"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude $*"
+mkdir -p build
+objs=()
+pids=()
+for s in $SRC; do
+  o=build/$(basename "$s").o
+  if [ ! -f "$o" ] || [ "$s" -nt "$o" ] || [ hcunet_amd/csrc/common.h -nt "$o" ] || [ include/hcunet.h -nt "$o" ] || [ build.sh -nt "$o" ]; then
+    lang=""
+    case "$s" in *.cpp) lang="-x hip";; esac
+    $HIPCC $lang $FLAGS -c "$s" -o "$o.tmp" && mv "$o.tmp" "$o" &
+    pids+=($!)
+  fi
+  objs+=("$o")
+done
+status=0
+for p in "${pids[@]:-}"; do
+  [ -z "$p" ] && continue
+  wait "$p" || status=1
+done
+if [ $status -ne 0 ]; then echo "build failed" >&2; exit 1; fi
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o "$OUT.tmp" "${objs[@]}"
+mv "$OUT.tmp" "$OUT"
+echo "built $OUT"

@@ -1,0 +1,145 @@
+"""ctypes binding of the C-ABI in include/hcunet.h (libhcunet.so, built in-tree).
+
+The library is the only compute path of this package: there is no CPU or
+PyTorch fallback.  If libhcunet.so is missing the first call raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhcunet.so")
+
+HCU_OK = 0
+HCU_ERR_INVALID = 1
+HCU_ERR_SHAPE = 2
+HCU_ERR_HIP = 3
+HCU_ERR_UNSUPPORTED = 4
+HCU_ERR_WORKSPACE = 5
+
+HCU_F32, HCU_F16, HCU_U8 = 0, 1, 2
+MAX_LEVELS = 12
+
+c_int3 = ctypes.c_int * 3
+
+
+class UnetSpec(ctypes.Structure):
+    _fields_ = [
+        ("levels", ctypes.c_int),
+        ("in_channels", ctypes.c_int),
+        ("out_channels", ctypes.c_int),
+        ("features", ctypes.c_int * MAX_LEVELS),
+        ("k1", c_int3), ("k2", c_int3),
+        ("d1", c_int3), ("d2", c_int3),
+        ("g1", ctypes.c_int), ("g2", ctypes.c_int),
+        ("up_k", c_int3), ("up_s", c_int3),
+        ("pool_k", c_int3),
+        ("bn_eps", ctypes.c_float),
+        ("bn_momentum", ctypes.c_float),
+    ]
+
+
+class UnetTensors(ctypes.Structure):
+    _fields_ = [
+        ("x", ctypes.c_void_p),
+        ("out", ctypes.c_void_p),
+        ("params", ctypes.c_void_p),
+        ("grads", ctypes.c_void_p),
+        ("bn_running_mean", ctypes.POINTER(ctypes.c_void_p)),
+        ("bn_running_var", ctypes.POINTER(ctypes.c_void_p)),
+        ("bn_num_batches_tracked", ctypes.POINTER(ctypes.c_void_p)),
+        ("saved", ctypes.c_void_p),
+        ("scratch", ctypes.c_void_p),
+    ]
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("Cin", ctypes.c_int), ("Cout", ctypes.c_int),
+        ("X", ctypes.c_int), ("Y", ctypes.c_int), ("Z", ctypes.c_int),
+        ("k", c_int3), ("stride", c_int3), ("dil", c_int3),
+        ("groups", ctypes.c_int),
+        ("transposed", ctypes.c_int),
+    ]
+
+
+# Every symbol include/hcunet.h declares: (name, restype, argtypes)
+_VP, _I, _I64, _F, _SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+SYMBOLS = [
+    ("hcu_last_error", ctypes.c_char_p, []),
+    ("hcu_version", _I, []),
+    ("hcu_unet_plan_create", _I, [ctypes.POINTER(UnetSpec), _I, _I, _I, _I, ctypes.POINTER(_VP)]),
+    ("hcu_unet_plan_destroy", None, [_VP]),
+    ("hcu_unet_plan_query", _I, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I64),
+                                 ctypes.POINTER(_I), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    ("hcu_unet_forward", _I, [_VP, ctypes.POINTER(UnetTensors), _I, _VP]),
+    ("hcu_unet_backward", _I, [_VP, ctypes.POINTER(UnetTensors), _VP, _VP, _I, _I, _VP]),
+    ("hcu_loss_pixel_scratch_bytes", _SZ, [_I64]),
+    ("hcu_loss_pixel_fwd", _I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _I, _I, _I,
+                                _VP, _VP, _VP, _SZ, _VP]),
+    ("hcu_scale_by_device_scalar", _I, [_VP, _VP, _VP, _I64, _VP]),
+    ("hcu_adam_step", _I, [_VP, _VP, _VP, _VP, _I64, _F, _F, _F, _F, _F, _I64, _F, _VP]),
+    ("hcu_conv_scratch_bytes", _SZ, [ctypes.POINTER(ConvDesc)]),
+    ("hcu_conv_out_dims", _I, [ctypes.POINTER(ConvDesc), ctypes.POINTER(_I)]),
+    ("hcu_conv_fwd_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    ("hcu_conv_dgrad_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _SZ, _VP]),
+    ("hcu_conv_wgrad_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    ("hcu_maxpool_fwd_cl", _I, [_I, _I, _I, _I, _I, ctypes.POINTER(_I), _VP, _VP, _VP]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libhcunet.so (once) and declare every exported signature."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "hcunet_amd: native library %s is missing; build it with ./build.sh "
+                "(or __graft_entry__.build()). There is no CPU fallback." % LIB_PATH)
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SYMBOLS:
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def last_error():
+    msg = lib().hcu_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(code, what=""):
+    """Map a C-ABI error code to the exception type the reference path raises."""
+    if code == HCU_OK:
+        return
+    msg = last_error()
+    if what:
+        msg = "%s: %s" % (what, msg)
+    if code == HCU_ERR_INVALID:
+        raise ValueError(msg)
+    if code == HCU_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+def stream_handle(device=None):
+    """hipStream_t of torch's current stream on `device`."""
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def require_device(t, what):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor, got %s" % (what, type(t)))
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            "hcunet_amd: %s is on %s; the MI355X path runs on ROCm devices only "
+            "(move the module and tensors with .to('cuda'))" % (what, t.device))

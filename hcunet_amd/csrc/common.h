@@ -1,0 +1,201 @@
+// Internal declarations shared by the HIP kernels and the C++ executor.
+// All activation tensors are channels-last fp32: [B][X][Y][Z][Cs], Cs = round_up(C, 4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace hcu {
+
+inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+inline size_t align_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
+
+// Thread-local error message (hcu_last_error()).
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define HCU_HIP(expr)                                                            \
+  do {                                                                           \
+    hipError_t e__ = (expr);                                                     \
+    if (e__ != hipSuccess)                                                       \
+      return ::hcu::fail(3, std::string(#expr) + ": " + hipGetErrorString(e__)); \
+  } while (0)
+
+#define HCU_CHECK_LAUNCH() HCU_HIP(hipGetLastError())
+
+// ---------------------------------------------------------------------------
+// Generic gather convolution (implicit GEMM on v_mfma_f32_16x16x4_f32):
+//   out[b, o*os + of, co] = sum_{t, ci} act(in[b, o*s + t*d - p, ci]) * w[t][ci][co] (+ bias)
+// act = identity or relu(x*scale[ci] + shift[ci]) (BatchNorm+ReLU of the
+// producer fused on load); positions outside the input read as 0 (post-act).
+// Covers Conv3d forward (s=1, p=0), Conv3d dgrad (full correlation with flipped
+// taps), ConvTranspose3d dgrad (strided) and ConvTranspose3d forward (one
+// launch per output phase).  Optional per-block BatchNorm partial statistics.
+// ---------------------------------------------------------------------------
+struct GConvArgs {
+  const float *in;
+  const float *in_scale, *in_shift;   // [ICs] or null
+  const float *w;                     // [T][ICs][CoutW]
+  const float *bias;                  // [Cout] or null
+  float *out;
+  float *stats;                       // [B*ntiles][CoutW][2] or null
+  int B, IX, IY, IZ, ICs;
+  int OX, OY, OZ;                     // computed output grid
+  int SX, SY, SZ, OCs, Cout, CoutW;   // stored tensor
+  int osx, osy, osz, ofx, ofy, ofz;   // store mapping
+  int KX, KY, KZ;
+  int sx, sy, sz, dx, dy, dz, px, py, pz;
+  // tiling (filled by plan_gconv)
+  int TX, TY, TZ, ntx, nty, ntz;
+  int HX, HY, HZ, P;
+  int CK, NSUB, MPW;
+  int lds_bytes;
+};
+// Chooses the tile and kernel variant; returns 0 or an error code.
+int plan_gconv(GConvArgs &a, int target_blocks);
+int launch_gconv(const GConvArgs &a, hipStream_t s);
+inline int gconv_rows(const GConvArgs &a) { return a.B * a.ntx * a.nty * a.ntz; }
+
+// ---------------------------------------------------------------------------
+// Weight gradient (implicit GEMM, split over the reduction grid):
+//   partial[kb][row][col] = sum_{p in block kb} A[p*as + t*ad - ap][ci] * G[p*gs + t*gd - gp][co]
+// taps_rows=1: row=(t,ci) col=co (Conv3d);  taps_rows=0: row=ci col=(t,co) (ConvTranspose3d).
+// bias_row (taps_rows only): row T*ACs is a ones-row -> sum_p G[p][co].
+// ---------------------------------------------------------------------------
+struct WGradArgs {
+  const float *A;
+  const float *a_scale, *a_shift;
+  const float *G;
+  float *partial;                     // [KB][Mtot][Ntot]
+  int B;
+  int AX, AY, AZ, ACs;
+  int GX, GY, GZ, GCs;
+  int PX, PY, PZ;
+  int KX, KY, KZ;
+  int asx, asy, asz, adx, ady, adz, apx, apy, apz;
+  int gsx, gsy, gsz, gdx, gdy, gdz, gpx, gpy, gpz;
+  int taps_rows, bias_row;
+  int Mtot, Ntot;
+  // tiling (filled by plan_wgrad)
+  int TX, TY, TZ, ntx, nty, ntz;
+  int HAX, HAY, HAZ, PA, HGX, HGY, HGZ, PG;
+  int CKA, CKG, mloc, nloc, MS, NS;
+  int mchunks, nchunks, KB;
+  int lds_bytes;
+};
+int plan_wgrad(WGradArgs &a, int target_blocks);
+int launch_wgrad(const WGradArgs &a, hipStream_t s);
+inline size_t wgrad_partial_floats(const WGradArgs &a) {
+  return (size_t)a.KB * a.Mtot * a.Ntot;
+}
+
+// Sum wgrad partials over KB and scatter into PyTorch-layout gradients.
+//  mode 0 (Conv3d): dw[o][c][t] for o<Cout, c<Cin_g; effective input channel
+//         e = (g(o)*Cin_g + c) % fold_mod (fold_mod = channels of U when the
+//         cat(U,U) fold is active, else a large number); db[o] from bias row.
+//  mode 1 (ConvTranspose3d): dw[ci][co][t].
+struct WGradFinalize {
+  const float *partial;
+  float *dw, *db;
+  int KB, Mtot, Ntot, T;
+  int mode;
+  int Cout, Cin_g, groups, fold_mod, ACs;   // conv
+  int Cin, CoutT, GCs;                      // convT
+  int accumulate;
+};
+int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Pointwise / reduction kernels (pointwise.hip)
+// ---------------------------------------------------------------------------
+// Per-layer BatchNorm coefficient block, each array padded to Cs with zeros.
+struct BNCoef {
+  float *scale, *shift, *mean, *invstd, *c1, *c0;  // [Cs] each
+};
+
+int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
+                           double count, const float *gamma, const float *beta,
+                           float *run_mean, float *run_var, int64_t *nbt,
+                           float eps, float momentum, int training, BNCoef coef,
+                           hipStream_t s);
+int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, double count,
+                           BNCoef coef, float *dgamma, float *dbeta, int training,
+                           int accumulate, hipStream_t s);
+
+int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
+                       float *p, int B, int X, int Y, int Z, int Cs,
+                       int kx, int ky, int kz, hipStream_t s);
+
+// dz = dA * [relu'(z)] in place; partials [R][Cs][2] of (sum dz, sum dz*xhat).
+int bwd_rows(int64_t nvox, int Cs);
+int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef,
+                               int64_t nvox, int Cs, float *part, int R,
+                               hipStream_t s);
+// dz from a max-pool gradient dP (argmax recomputed from y).
+int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef,
+                              float *dz, int B, int X, int Y, int Z, int Cs,
+                              int kx, int ky, int kz, float *part, int R,
+                              hipStream_t s);
+// dy = dz*scale + c1*y + c0 in place.
+int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox,
+                        int Cs, hipStream_t s);
+
+// out_conv (1x1x1 Conv3d) forward: pred[b][o][v] (NCXYZ).
+int launch_outconv_fwd(const float *y, BNCoef coef, const float *w,
+                       const float *bias, float *pred, int B, int64_t V, int C,
+                       int Cs, int Co, hipStream_t s);
+// out_conv backward fused with the last BatchNorm's backward reduction.
+int outconv_bwd_rows(int64_t nvox, int Cs);
+int launch_outconv_bwd(const float *dpred, const float *y, BNCoef coef,
+                       const float *w, float *dz, int B, int64_t V, int C,
+                       int Cs, int Co, float *part_bn, float *part_oc, int R,
+                       hipStream_t s);
+
+// Channel sum of a channels-last tensor: partial [R][Cs].
+int chansum_rows(int64_t nvox, int Cs);
+int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R,
+                   hipStream_t s);
+// out[j] (=|+=) sum_r part[r*W + j] for j < n, mapped: out index = j (dense).
+int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
+                           int accumulate, hipStream_t s);
+
+// Layout: NCXYZ <-> channels-last (padded channels written as 0).
+int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V,
+                 hipStream_t s);
+int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V,
+                   hipStream_t s);
+
+// Weight preparation (PyTorch layout -> GEMM layouts).
+// Conv3d fwd:   wg[t][e][co] (e < ECs, co < CoutW)
+// Conv3d dgrad: wg[t'][co][e] (co < OCs, e < EW), t' = T-1-t
+int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int groups,
+                         int fold_mod, int T, int ECs, int CoutW, hipStream_t s);
+int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g,
+                           int groups, int fold_mod, int T, int OCs, int EW,
+                           int E, hipStream_t s);
+// ConvTranspose3d fwd phase (px,py,pz): wg[t][ci][co], t over (Jx,Jy,Jz) taps
+int launch_prep_convt_fwd(const float *w, float *wg, int Cin, int Cout, int KX,
+                          int KY, int KZ, int sx, int sy, int sz, int px, int py,
+                          int pz, int Jx, int Jy, int Jz, int ICs, int CoutW,
+                          hipStream_t s);
+// ConvTranspose3d dgrad: wg[t][co][ci] (co < UCs, ci < CinW)
+int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T,
+                            int UCs, int CinW, hipStream_t s);
+
+// Loss / optimizer (loss_adam.hip)
+int launch_loss_pixel(const float *pred, int B, int C, int PX, int PY, int PZ,
+                      const void *mask, int mask_dtype, const void *pwl,
+                      int pwl_dtype, int MX, int MY, int MZ, float *loss,
+                      float *dpred, float *part, int R, hipStream_t s);
+int loss_rows(int64_t n);
+int launch_scale(const float *src, const float *scale, float *dst, int64_t n,
+                 hipStream_t s);
+int launch_adam(float *p, const float *g, float *m, float *v, int64_t n, float lr,
+                float b1, float b2, float eps, float wd, int64_t step,
+                float grad_scale, hipStream_t s);
+
+}  // namespace hcu

@@ -1,0 +1,792 @@
+// HBM-bound kernels of the U-Net step: BatchNorm3d statistics finalisation
+// (nn.BatchNorm3d train/eval semantics, hcat/unet.py:259-260,305-306),
+// MaxPool3d forward/backward (hcat/unet.py:123,131), the BatchNorm+ReLU
+// backward reductions, the out_conv 1x1x1 Conv3d (hcat/unet.py:120,138),
+// NCXYZ <-> channels-last layout changes and the weight re-layouts feeding the
+// implicit-GEMM kernels.
+//
+// Every reduction writes fixed-size per-workgroup partial rows that a second
+// kernel sums in fp64 in a fixed order: results are bitwise reproducible run to
+// run (no float atomics anywhere).
+#include "common.h"
+#include <algorithm>
+
+namespace hcu {
+
+__device__ __forceinline__ float bnrelu(float y, float sc, float sh) {
+  return fmaxf(fmaf(y, sc, sh), 0.f);
+}
+__device__ __forceinline__ float4 ld4(const float *p) {
+  return *reinterpret_cast<const float4 *>(p);
+}
+__device__ __forceinline__ void st4(float *p, float4 v) {
+  *reinterpret_cast<float4 *>(p) = v;
+}
+__device__ __forceinline__ float comp(const float4 &v, int j) {
+  return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm forward finalisation: one workgroup per channel.
+__global__ void __launch_bounds__(256)
+bn_fwd_finalize_kernel(const float *stats, int R, int W, int C, double count,
+                       const float *gamma, const float *beta, float *rm, float *rv,
+                       const int64_t *nbt, float eps, float momentum, int training,
+                       BNCoef coef) {
+  __shared__ double r1[256], r2[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  if (training && c < C) {
+    for (int r = tid; r < R; r += 256) {
+      s1 += (double)stats[((size_t)r * W + c) * 2 + 0];
+      s2 += (double)stats[((size_t)r * W + c) * 2 + 1];
+    }
+  }
+  r1[tid] = s1;
+  r2[tid] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+      r1[tid] += r1[tid + off];
+      r2[tid] += r2[tid + off];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  if (c >= C) {
+    coef.scale[c] = coef.shift[c] = coef.mean[c] = coef.invstd[c] = 0.f;
+    coef.c1[c] = coef.c0[c] = 0.f;
+    return;
+  }
+  float mean, invstd;
+  if (training) {
+    const double m = r1[0] / count;
+    double v = r2[0] / count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    invstd = (float)(1.0 / sqrt(v + (double)eps));
+    if (rm) {
+      const double f = momentum >= 0.f ? (double)momentum : 1.0 / (double)(nbt[0] + 1);
+      const double unb = count > 1.0 ? v * count / (count - 1.0) : v;
+      rm[c] = (float)(f * m + (1.0 - f) * (double)rm[c]);
+      rv[c] = (float)(f * unb + (1.0 - f) * (double)rv[c]);
+    }
+  } else {
+    mean = rm[c];
+    invstd = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+  }
+  const float g = gamma ? gamma[c] : 1.f;
+  const float bb = beta ? beta[c] : 0.f;
+  const float sc = g * invstd;
+  coef.scale[c] = sc;
+  coef.shift[c] = bb - mean * sc;
+  coef.mean[c] = mean;
+  coef.invstd[c] = invstd;
+}
+
+int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
+                           double count, const float *gamma, const float *beta,
+                           float *run_mean, float *run_var, int64_t *nbt,
+                           float eps, float momentum, int training, BNCoef coef,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, stats, R,
+                     statsW, C, count, gamma, beta, run_mean, run_var, nbt, eps,
+                     momentum, training, coef);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// BatchNorm backward finalisation: per channel sum dz and sum dz*xhat.
+__global__ void __launch_bounds__(256)
+bn_bwd_finalize_kernel(const float *part, int R, int C, int Cs, double count,
+                       BNCoef coef, float *dgamma, float *dbeta, int training,
+                       int accumulate) {
+  __shared__ double r1[256], r2[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (int r = tid; r < R; r += 256) {
+      s1 += (double)part[((size_t)r * Cs + c) * 2 + 0];
+      s2 += (double)part[((size_t)r * Cs + c) * 2 + 1];
+    }
+  }
+  r1[tid] = s1;
+  r2[tid] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+      r1[tid] += r1[tid + off];
+      r2[tid] += r2[tid + off];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  if (c >= C) {
+    coef.c1[c] = coef.c0[c] = 0.f;
+    return;
+  }
+  const double db = r1[0], dg = r2[0];
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)db : (float)db;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)dg : (float)dg;
+  if (training) {
+    const double sc = coef.scale[c], is = coef.invstd[c], mu = coef.mean[c];
+    const double c1 = -sc * is * dg / count;
+    const double c0 = -sc * db / count - c1 * mu;
+    coef.c1[c] = (float)c1;
+    coef.c0[c] = (float)c0;
+  } else {
+    coef.c1[c] = 0.f;
+    coef.c0[c] = 0.f;
+  }
+}
+
+int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, double count,
+                           BNCoef coef, float *dgamma, float *dbeta, int training,
+                           int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, part, R, C,
+                     Cs, count, coef, dgamma, dbeta, training, accumulate);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// MaxPool3d forward on relu(bn(y)), kernel == stride, floor mode.
+__global__ void __launch_bounds__(256)
+maxpool_fwd_kernel(const float *y, const float *scale, const float *shift, float *p,
+                   int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
+                   int PX, int PY, int PZ) {
+  const int C4 = Cs / 4;
+  const int64_t n = (int64_t)B * PX * PY * PZ * C4;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n;
+       idx += (int64_t)gridDim.x * 256) {
+    const int c4 = (int)(idx % C4);
+    int64_t v = idx / C4;
+    const int pz = (int)(v % PZ);
+    v /= PZ;
+    const int py = (int)(v % PY);
+    v /= PY;
+    const int px = (int)(v % PX);
+    const int b = (int)(v / PX);
+    const int c = c4 * 4;
+    float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (scale) {
+      sc = ld4(scale + c);
+      sh = ld4(shift + c);
+    }
+    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    for (int i = 0; i < kx; ++i)
+      for (int j = 0; j < ky; ++j)
+        for (int k = 0; k < kz; ++k) {
+          const int x = px * kx + i, yy = py * ky + j, z = pz * kz + k;
+          const float4 t = ld4(y + ((((size_t)b * X + x) * Y + yy) * Z + z) * Cs + c);
+          float4 a;
+          if (scale) {
+            a.x = bnrelu(t.x, sc.x, sh.x);
+            a.y = bnrelu(t.y, sc.y, sh.y);
+            a.z = bnrelu(t.z, sc.z, sh.z);
+            a.w = bnrelu(t.w, sc.w, sh.w);
+          } else {
+            a = t;
+          }
+          m.x = a.x > m.x ? a.x : m.x;
+          m.y = a.y > m.y ? a.y : m.y;
+          m.z = a.z > m.z ? a.z : m.z;
+          m.w = a.w > m.w ? a.w : m.w;
+        }
+    st4(p + ((((size_t)b * PX + px) * PY + py) * PZ + pz) * Cs + c, m);
+  }
+}
+
+static int grid_for(int64_t n) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
+}
+
+int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
+                       float *p, int B, int X, int Y, int Z, int Cs, int kx, int ky,
+                       int kz, hipStream_t s) {
+  const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
+  const int64_t n = (int64_t)B * PX * PY * PZ * (Cs / 4);
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, scale,
+                     shift, p, B, X, Y, Z, Cs, kx, ky, kz, PX, PY, PZ);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Row partitioning shared by the per-channel reductions: workgroup r handles
+// the element range [r*chunk, (r+1)*chunk) of the (voxel, channel-quad) space.
+struct RedGeom {
+  int tb;          // threads per workgroup (multiple of C4)
+  int64_t chunk;   // elements per workgroup (multiple of tb)
+  int64_t total;
+};
+__host__ __device__ inline RedGeom red_geom(int64_t nvox, int Cs, int R) {
+  RedGeom g;
+  const int C4 = Cs / 4;
+  g.tb = C4 <= 256 ? (256 / C4) * C4 : C4;
+  g.total = nvox * C4;
+  int64_t per = (g.total + R - 1) / R;
+  g.chunk = (per + g.tb - 1) / g.tb * g.tb;
+  return g;
+}
+int bwd_rows(int64_t nvox, int Cs) {
+  const int C4 = Cs / 4;
+  const int tb = C4 <= 256 ? (256 / C4) * C4 : C4;
+  const int64_t total = nvox * C4;
+  int64_t r = (total + (int64_t)tb * 4 - 1) / ((int64_t)tb * 4);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(r, 1024));
+}
+int chansum_rows(int64_t nvox, int Cs) { return bwd_rows(nvox, Cs); }
+int outconv_bwd_rows(int64_t nvox, int Cs) { return bwd_rows(nvox, Cs); }
+
+// Fixed-order block reduction of NV floats per thread, grouped by c4.
+template <int NV>
+__device__ void block_reduce_c4(float (&v)[NV], float *lds, int tb, int C4,
+                                float *out_row /* [C4][NV] */) {
+  const int tid = threadIdx.x;
+  if (tid < tb)
+    for (int k = 0; k < NV; ++k) lds[tid * NV + k] = v[k];
+  __syncthreads();
+  if (tid < C4) {
+    float acc[NV];
+    for (int k = 0; k < NV; ++k) acc[k] = 0.f;
+    for (int t = tid; t < tb; t += C4)
+      for (int k = 0; k < NV; ++k) acc[k] += lds[t * NV + k];
+    for (int k = 0; k < NV; ++k) out_row[tid * NV + k] = acc[k];
+  }
+}
+
+// dz = dA * [z > 0] in place, partial (sum dz, sum dz*xhat) per channel.
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_dense_kernel(float *dA, const float *y, BNCoef coef, int64_t nvox,
+                           int Cs, float *part, RedGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int C4 = Cs / 4, tid = threadIdx.x;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (tid < g.tb) {
+    const int64_t beg = (int64_t)blockIdx.x * g.chunk;
+    const int64_t end = std::min(beg + g.chunk, g.total);
+    const int c = (int)((beg + tid) % C4) * 4;
+    const float4 sc = ld4(coef.scale + c), sh = ld4(coef.shift + c);
+    const float4 mu = ld4(coef.mean + c), is = ld4(coef.invstd + c);
+    for (int64_t e = beg + tid; e < end; e += g.tb) {
+      const int64_t vox = e / C4;
+      const size_t off = (size_t)vox * Cs + c;
+      const float4 yy = ld4(y + off);
+      float4 d = ld4(dA + off);
+      d.x = fmaf(yy.x, sc.x, sh.x) > 0.f ? d.x : 0.f;
+      d.y = fmaf(yy.y, sc.y, sh.y) > 0.f ? d.y : 0.f;
+      d.z = fmaf(yy.z, sc.z, sh.z) > 0.f ? d.z : 0.f;
+      d.w = fmaf(yy.w, sc.w, sh.w) > 0.f ? d.w : 0.f;
+      st4(dA + off, d);
+      v[0] += d.x;
+      v[1] = fmaf(d.x, (yy.x - mu.x) * is.x, v[1]);
+      v[2] += d.y;
+      v[3] = fmaf(d.y, (yy.y - mu.y) * is.y, v[3]);
+      v[4] += d.z;
+      v[5] = fmaf(d.z, (yy.z - mu.z) * is.z, v[5]);
+      v[6] += d.w;
+      v[7] = fmaf(d.w, (yy.w - mu.w) * is.w, v[7]);
+    }
+  }
+  block_reduce_c4<8>(v, lds, g.tb, C4, part + (size_t)blockIdx.x * Cs * 2);
+}
+
+int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef, int64_t nvox,
+                               int Cs, float *part, int R, hipStream_t s) {
+  const RedGeom g = red_geom(nvox, Cs, R);
+  hipLaunchKernelGGL(bn_bwd_reduce_dense_kernel, dim3(R), dim3(256),
+                     (size_t)std::max(g.tb, 256) * 8 * 4, s, dA, y, coef, nvox, Cs, part, g);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// Max-pool backward (argmax recomputed from y, first maximum in x,y,z window
+// order as torch's CPU max_pool3d) fused with the BatchNorm+ReLU reduction.
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_pool_kernel(const float *dP, const float *y, BNCoef coef, float *dz,
+                          int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
+                          float *part, RedGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int C4 = Cs / 4, tid = threadIdx.x;
+  const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (tid < g.tb) {
+    const int64_t beg = (int64_t)blockIdx.x * g.chunk;
+    const int64_t end = std::min(beg + g.chunk, g.total);
+    const int c = (int)((beg + tid) % C4) * 4;
+    const float4 sc = ld4(coef.scale + c), sh = ld4(coef.shift + c);
+    const float4 mu = ld4(coef.mean + c), is = ld4(coef.invstd + c);
+    for (int64_t e = beg + tid; e < end; e += g.tb) {
+      int64_t vox = e / C4;
+      const size_t off = (size_t)vox * Cs + c;
+      const int z = (int)(vox % Z);
+      vox /= Z;
+      const int yy = (int)(vox % Y);
+      vox /= Y;
+      const int x = (int)(vox % X);
+      const int b = (int)(vox / X);
+      const float4 yv = ld4(y + off);
+      const float4 zv = make_float4(fmaf(yv.x, sc.x, sh.x), fmaf(yv.y, sc.y, sh.y),
+                                    fmaf(yv.z, sc.z, sh.z), fmaf(yv.w, sc.w, sh.w));
+      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int wx = x / kx, wy = yy / ky, wz = z / kz;
+      if (wx < PX && wy < PY && wz < PZ) {
+        float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+        int4 am = make_int4(-1, -1, -1, -1);
+        int idx = 0;
+        for (int i = 0; i < kx; ++i)
+          for (int j = 0; j < ky; ++j)
+            for (int k = 0; k < kz; ++k, ++idx) {
+              const float4 t = ld4(
+                  y + ((((size_t)b * X + wx * kx + i) * Y + wy * ky + j) * Z + wz * kz + k) * Cs + c);
+              const float a0 = bnrelu(t.x, sc.x, sh.x), a1 = bnrelu(t.y, sc.y, sh.y);
+              const float a2 = bnrelu(t.z, sc.z, sh.z), a3 = bnrelu(t.w, sc.w, sh.w);
+              if (a0 > m.x) { m.x = a0; am.x = idx; }
+              if (a1 > m.y) { m.y = a1; am.y = idx; }
+              if (a2 > m.z) { m.z = a2; am.z = idx; }
+              if (a3 > m.w) { m.w = a3; am.w = idx; }
+            }
+        const int own = ((x - wx * kx) * ky + (yy - wy * ky)) * kz + (z - wz * kz);
+        const float4 gp = ld4(dP + ((((size_t)b * PX + wx) * PY + wy) * PZ + wz) * Cs + c);
+        d.x = (am.x == own && zv.x > 0.f) ? gp.x : 0.f;
+        d.y = (am.y == own && zv.y > 0.f) ? gp.y : 0.f;
+        d.z = (am.z == own && zv.z > 0.f) ? gp.z : 0.f;
+        d.w = (am.w == own && zv.w > 0.f) ? gp.w : 0.f;
+      }
+      st4(dz + off, d);
+      v[0] += d.x;
+      v[1] = fmaf(d.x, (yv.x - mu.x) * is.x, v[1]);
+      v[2] += d.y;
+      v[3] = fmaf(d.y, (yv.y - mu.y) * is.y, v[3]);
+      v[4] += d.z;
+      v[5] = fmaf(d.z, (yv.z - mu.z) * is.z, v[5]);
+      v[6] += d.w;
+      v[7] = fmaf(d.w, (yv.w - mu.w) * is.w, v[7]);
+    }
+  }
+  block_reduce_c4<8>(v, lds, g.tb, C4, part + (size_t)blockIdx.x * Cs * 2);
+}
+
+int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, float *dz,
+                              int B, int X, int Y, int Z, int Cs, int kx, int ky,
+                              int kz, float *part, int R, hipStream_t s) {
+  const RedGeom g = red_geom((int64_t)B * X * Y * Z, Cs, R);
+  hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
+                     (size_t)std::max(g.tb, 256) * 8 * 4, s, dP, y, coef, dz, B, X, Y, Z,
+                     Cs, kx, ky, kz, part, g);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// dy = dz*scale + c1*y + c0, in place.
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_kernel(float *dz, const float *y, BNCoef coef, int64_t n4, int C4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C4) * 4;
+    const float4 sc = ld4(coef.scale + c), c1 = ld4(coef.c1 + c), c0 = ld4(coef.c0 + c);
+    const float4 yy = ld4(y + i * 4);
+    float4 d = ld4(dz + i * 4);
+    d.x = fmaf(d.x, sc.x, fmaf(c1.x, yy.x, c0.x));
+    d.y = fmaf(d.y, sc.y, fmaf(c1.y, yy.y, c0.y));
+    d.z = fmaf(d.z, sc.z, fmaf(c1.z, yy.z, c0.z));
+    d.w = fmaf(d.w, sc.w, fmaf(c1.w, yy.w, c0.w));
+    st4(dz + i * 4, d);
+  }
+}
+
+int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, int Cs,
+                        hipStream_t s) {
+  const int64_t n4 = nvox * (Cs / 4);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, s, dz, y,
+                     coef, n4, Cs / 4);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// out_conv forward: pred[b][o][v] = sum_c relu(bn(y))[v][c] * w[o][c] + bias[o]
+#define MAXCO 4
+__global__ void __launch_bounds__(256)
+outconv_fwd_kernel(const float *y, BNCoef coef, const float *w, const float *bias,
+                   float *pred, int B, int64_t V, int C, int Cs, int Co) {
+  const int64_t n = (int64_t)B * V;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int b = (int)(i / V);
+    const int64_t v = i % V;
+    float acc[MAXCO];
+    for (int o = 0; o < MAXCO; ++o) acc[o] = 0.f;
+    const float *yr = y + (size_t)i * Cs;
+    for (int c0 = 0; c0 < Cs; c0 += 4) {
+      const float4 yy = ld4(yr + c0);
+      const float4 sc = ld4(coef.scale + c0), sh = ld4(coef.shift + c0);
+      const float a[4] = {bnrelu(yy.x, sc.x, sh.x), bnrelu(yy.y, sc.y, sh.y),
+                          bnrelu(yy.z, sc.z, sh.z), bnrelu(yy.w, sc.w, sh.w)};
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        if (c < C)
+          for (int o = 0; o < Co && o < MAXCO; ++o) acc[o] = fmaf(a[j], w[o * C + c], acc[o]);
+      }
+    }
+    for (int o = 0; o < Co && o < MAXCO; ++o)
+      pred[((size_t)b * Co + o) * V + v] = acc[o] + (bias ? bias[o] : 0.f);
+  }
+}
+
+int launch_outconv_fwd(const float *y, BNCoef coef, const float *w, const float *bias,
+                       float *pred, int B, int64_t V, int C, int Cs, int Co,
+                       hipStream_t s) {
+  if (Co > MAXCO) return fail(4, "out_conv: out_channels > 4 not supported");
+  hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for((int64_t)B * V)), dim3(256), 0, s,
+                     y, coef, w, bias, pred, B, V, C, Cs, Co);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// out_conv backward + last BatchNorm backward reduction.
+//   dA[v][c] = sum_o dpred[o][v] w[o][c];  dz = dA [z>0];
+//   part_bn[r][c][2] = (sum dz, sum dz*xhat);
+//   part_oc[r][o*Cs + c] = sum dpred[o] a[c];  part_oc[r][Co*Cs + o] = sum dpred[o]
+__global__ void __launch_bounds__(256)
+outconv_bwd_kernel(const float *dpred, const float *y, BNCoef coef, const float *w,
+                   float *dz, int B, int64_t V, int C, int Cs, int Co, float *part_bn,
+                   float *part_oc, RedGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NV = 8 + 5 * MAXCO;
+  const int C4 = Cs / 4, tid = threadIdx.x;
+  float v[NV];
+  for (int k = 0; k < NV; ++k) v[k] = 0.f;
+  if (tid < g.tb) {
+    const int64_t beg = (int64_t)blockIdx.x * g.chunk;
+    const int64_t end = std::min(beg + g.chunk, g.total);
+    const int c = (int)((beg + tid) % C4) * 4;
+    const float4 sc = ld4(coef.scale + c), sh = ld4(coef.shift + c);
+    const float4 mu = ld4(coef.mean + c), is = ld4(coef.invstd + c);
+    float wv[MAXCO][4];
+    for (int o = 0; o < MAXCO; ++o)
+      for (int j = 0; j < 4; ++j) wv[o][j] = (o < Co && c + j < C) ? w[o * C + c + j] : 0.f;
+    for (int64_t e = beg + tid; e < end; e += g.tb) {
+      const int64_t vox = e / C4;
+      const int b = (int)(vox / V);
+      const int64_t vv = vox % V;
+      const size_t off = (size_t)vox * Cs + c;
+      const float4 yy = ld4(y + off);
+      float dp[MAXCO];
+      for (int o = 0; o < MAXCO; ++o) dp[o] = o < Co ? dpred[((size_t)b * Co + o) * V + vv] : 0.f;
+      const float yv[4] = {yy.x, yy.y, yy.z, yy.w};
+      const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+      const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+      float dzv[4];
+      for (int j = 0; j < 4; ++j) {
+        const float z = fmaf(yv[j], scv[j], shv[j]);
+        const float a = fmaxf(z, 0.f);
+        float dA = 0.f;
+        for (int o = 0; o < MAXCO; ++o) {
+          dA = fmaf(dp[o], wv[o][j], dA);
+          v[8 + o * 4 + j] = fmaf(dp[o], a, v[8 + o * 4 + j]);
+        }
+        dzv[j] = z > 0.f ? dA : 0.f;
+        v[2 * j] += dzv[j];
+        v[2 * j + 1] = fmaf(dzv[j], (yv[j] - muv[j]) * isv[j], v[2 * j + 1]);
+      }
+      if (c == 0)
+        for (int o = 0; o < MAXCO; ++o) v[8 + 4 * MAXCO + o] += dp[o];
+      st4(dz + off, make_float4(dzv[0], dzv[1], dzv[2], dzv[3]));
+    }
+  }
+  // reduce per c4 group
+  if (tid < g.tb)
+    for (int k = 0; k < NV; ++k) lds[tid * NV + k] = v[k];
+  __syncthreads();
+  if (tid < C4) {
+    float acc[NV];
+    for (int k = 0; k < NV; ++k) acc[k] = 0.f;
+    for (int t = tid; t < g.tb; t += C4)
+      for (int k = 0; k < NV; ++k) acc[k] += lds[t * NV + k];
+    const int c = tid * 4;
+    float *pb = part_bn + (size_t)blockIdx.x * Cs * 2;
+    for (int k = 0; k < 8; ++k) pb[c * 2 + k] = acc[k];
+    float *po = part_oc + (size_t)blockIdx.x * (Co * Cs + Co);
+    for (int o = 0; o < Co; ++o)
+      for (int j = 0; j < 4; ++j) po[o * Cs + c + j] = acc[8 + o * 4 + j];
+    if (tid == 0)
+      for (int o = 0; o < Co; ++o) po[Co * Cs + o] = acc[8 + 4 * MAXCO + o];
+  }
+}
+
+int launch_outconv_bwd(const float *dpred, const float *y, BNCoef coef, const float *w,
+                       float *dz, int B, int64_t V, int C, int Cs, int Co, float *part_bn,
+                       float *part_oc, int R, hipStream_t s) {
+  if (Co > MAXCO) return fail(4, "out_conv: out_channels > 4 not supported");
+  const RedGeom g = red_geom((int64_t)B * V, Cs, R);
+  const size_t lds = (size_t)std::max(g.tb, 256) * (8 + 5 * MAXCO) * 4;
+  hipLaunchKernelGGL(outconv_bwd_kernel, dim3(R), dim3(256), lds, s, dpred, y, coef, w,
+                     dz, B, V, C, Cs, Co, part_bn, part_oc, g);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+chansum_kernel(const float *x, int Cs, float *part, RedGeom g) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int C4 = Cs / 4, tid = threadIdx.x;
+  float v[4] = {0, 0, 0, 0};
+  if (tid < g.tb) {
+    const int64_t beg = (int64_t)blockIdx.x * g.chunk;
+    const int64_t end = std::min(beg + g.chunk, g.total);
+    for (int64_t e = beg + tid; e < end; e += g.tb) {
+      const float4 t = ld4(x + e * 4);
+      v[0] += t.x;
+      v[1] += t.y;
+      v[2] += t.z;
+      v[3] += t.w;
+    }
+  }
+  block_reduce_c4<4>(v, lds, g.tb, C4, part + (size_t)blockIdx.x * Cs);
+}
+
+int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R, hipStream_t s) {
+  const RedGeom g = red_geom(nvox, Cs, R);
+  hipLaunchKernelGGL(chansum_kernel, dim3(R), dim3(256), (size_t)std::max(g.tb, 256) * 4 * 4,
+                     s, x, Cs, part, g);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+reduce_partials_kernel(const float *part, int R, int W, int n, float *out, int accumulate) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += (double)part[(size_t)r * W + j];
+  out[j] = accumulate ? out[j] + (float)s : (float)s;
+}
+
+int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
+                           int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, R,
+                     W, n, out, accumulate);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+to_cl_kernel(const float *x, float *xcl, int B, int C, int Cs, int64_t V) {
+  const int C4 = Cs / 4;
+  const int64_t n = (int64_t)B * C4 * V;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t v = i % V;
+    const int64_t q = i / V;
+    const int c4 = (int)(q % C4);
+    const int b = (int)(q / C4);
+    float r[4];
+    for (int j = 0; j < 4; ++j) {
+      const int c = c4 * 4 + j;
+      r[j] = c < C ? x[((size_t)b * C + c) * V + v] : 0.f;
+    }
+    st4(xcl + ((size_t)b * V + v) * Cs + c4 * 4, make_float4(r[0], r[1], r[2], r[3]));
+  }
+}
+
+int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s) {
+  const int64_t n = (int64_t)B * (Cs / 4) * V;
+  hipLaunchKernelGGL(to_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xcl, B, C, Cs, V);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+from_cl_kernel(const float *xcl, float *x, int B, int C, int Cs, int64_t V) {
+  const int64_t n = (int64_t)B * C * V;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t v = i % V;
+    const int64_t q = i / V;
+    const int c = (int)(q % C);
+    const int b = (int)(q / C);
+    x[i] = xcl[((size_t)b * V + v) * Cs + c];
+  }
+}
+
+int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V, hipStream_t s) {
+  const int64_t n = (int64_t)B * C * V;
+  hipLaunchKernelGGL(from_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, xcl, x, B, C, Cs, V);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Effective (folded, block-diagonal) Conv3d weight element W_eff[o][e][t].
+__device__ inline float weff(const float *w, int o, int e, int t, int Cout, int Cin_g,
+                             int groups, int fold_mod, int T) {
+  const int g = o / (Cout / groups);
+  const int cin_total = groups * Cin_g;
+  float s = 0.f;
+  for (int cp = e; cp < cin_total; cp += fold_mod) {
+    const int c = cp - g * Cin_g;
+    if (c >= 0 && c < Cin_g) s += w[((size_t)o * Cin_g + c) * T + t];
+  }
+  return s;
+}
+
+__global__ void __launch_bounds__(256)
+prep_conv_fwd_kernel(const float *w, float *wg, int Cout, int Cin_g, int groups,
+                     int fold_mod, int T, int ECs, int CoutW, int E) {
+  const int64_t n = (int64_t)T * ECs * CoutW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int co = (int)(i % CoutW);
+    const int64_t q = i / CoutW;
+    const int e = (int)(q % ECs);
+    const int t = (int)(q / ECs);
+    wg[i] = (co < Cout && e < E) ? weff(w, co, e, t, Cout, Cin_g, groups, fold_mod, T) : 0.f;
+  }
+}
+
+int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int groups,
+                         int fold_mod, int T, int ECs, int CoutW, hipStream_t s) {
+  const int E = std::min(fold_mod, groups * Cin_g);
+  const int64_t n = (int64_t)T * ECs * CoutW;
+  hipLaunchKernelGGL(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
+                     Cin_g, groups, fold_mod, T, ECs, CoutW, E);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+prep_conv_dgrad_kernel(const float *w, float *wg, int Cout, int Cin_g, int groups,
+                       int fold_mod, int T, int OCs, int EW, int E) {
+  const int64_t n = (int64_t)T * OCs * EW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int e = (int)(i % EW);
+    const int64_t q = i / EW;
+    const int co = (int)(q % OCs);
+    const int tp = (int)(q / OCs);
+    wg[i] = (co < Cout && e < E)
+                ? weff(w, co, e, T - 1 - tp, Cout, Cin_g, groups, fold_mod, T)
+                : 0.f;
+  }
+}
+
+int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g, int groups,
+                           int fold_mod, int T, int OCs, int EW, int E, hipStream_t s) {
+  const int64_t n = (int64_t)T * OCs * EW;
+  hipLaunchKernelGGL(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
+                     Cin_g, groups, fold_mod, T, OCs, EW, E);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+prep_convt_fwd_kernel(const float *w, float *wg, int Cin, int Cout, int KX, int KY, int KZ,
+                      int sx, int sy, int sz, int px, int py, int pz, int Jx, int Jy,
+                      int Jz, int ICs, int CoutW) {
+  const int Tp = Jx * Jy * Jz;
+  const int64_t n = (int64_t)Tp * ICs * CoutW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int co = (int)(i % CoutW);
+    const int64_t q = i / CoutW;
+    const int ci = (int)(q % ICs);
+    const int t = (int)(q / ICs);
+    const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
+    const int kx = px + sx * (Jx - 1 - tx), ky = py + sy * (Jy - 1 - ty),
+              kz = pz + sz * (Jz - 1 - tz);
+    float v = 0.f;
+    if (ci < Cin && co < Cout && kx < KX && ky < KY && kz < KZ)
+      v = w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
+    wg[i] = v;
+  }
+}
+
+int launch_prep_convt_fwd(const float *w, float *wg, int Cin, int Cout, int KX, int KY,
+                          int KZ, int sx, int sy, int sz, int px, int py, int pz, int Jx,
+                          int Jy, int Jz, int ICs, int CoutW, hipStream_t s) {
+  const int64_t n = (int64_t)Jx * Jy * Jz * ICs * CoutW;
+  hipLaunchKernelGGL(prep_convt_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
+                     Cout, KX, KY, KZ, sx, sy, sz, px, py, pz, Jx, Jy, Jz, ICs, CoutW);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+prep_convt_dgrad_kernel(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
+                        int CinW) {
+  const int64_t n = (int64_t)T * UCs * CinW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const int ci = (int)(i % CinW);
+    const int64_t q = i / CinW;
+    const int co = (int)(q % UCs);
+    const int t = (int)(q / UCs);
+    wg[i] = (ci < Cin && co < Cout) ? w[((size_t)ci * Cout + co) * T + t] : 0.f;
+  }
+}
+
+int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
+                            int CinW, hipStream_t s) {
+  const int64_t n = (int64_t)T * UCs * CinW;
+  hipLaunchKernelGGL(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
+                     Cout, T, UCs, CinW);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// out_conv weight/bias gradient from the fused backward's partial rows.
+__global__ void __launch_bounds__(256)
+outconv_wfinalize_kernel(const float *part, int R, int Co, int C, int Cs, float *dw, float *db,
+                         int accumulate) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int W = Co * Cs + Co;
+  if (j >= Co * C + Co) return;
+  int src;
+  float *dst;
+  if (j < Co * C) {
+    const int o = j / C, c = j % C;
+    src = o * Cs + c;
+    dst = dw + j;
+  } else {
+    src = Co * Cs + (j - Co * C);
+    dst = db + (j - Co * C);
+  }
+  double s = 0.0;
+  for (int r = 0; r < R; ++r) s += (double)part[(size_t)r * W + src];
+  *dst = accumulate ? *dst + (float)s : (float)s;
+}
+
+int launch_outconv_wfinalize(const float *part_oc, int R, int Co, int C, int Cs, float *dw,
+                             float *db, int accumulate, hipStream_t s) {
+  const int n = Co * C + Co;
+  hipLaunchKernelGGL(outconv_wfinalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part_oc,
+                     R, Co, C, Cs, dw, db, accumulate);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+// num_batches_tracked += 1 for every BatchNorm3d of the net (train forward).
+struct CountPtrs {
+  int64_t *p[64];
+  int n;
+};
+__global__ void bn_count_kernel(CountPtrs c) {
+  const int i = threadIdx.x;
+  if (i < c.n && c.p[i]) c.p[i][0] += 1;
+}
+
+int launch_bn_count_increment(int64_t *const *ptrs, int n, hipStream_t s) {
+  if (n > 64) return fail(4, "too many BatchNorm layers");
+  CountPtrs c{};
+  for (int i = 0; i < n; ++i) c.p[i] = ptrs[i];
+  c.n = n;
+  hipLaunchKernelGGL(bn_count_kernel, dim3(1), dim3(64), 0, s, c);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu

@@ -1,0 +1,986 @@
+// Native executor for the 3D U-Net training hot path.
+//
+// A plan is built once per (spec, input shape): it resolves every layer's
+// shapes exactly as hcat.unet.Unet_Constructor would see them
+// (hcat/unet.py:16-143), reports the errors torch would raise, picks the
+// kernel tiles, and lays out two caller-owned workspaces:
+//   saved   - what backward needs from forward: the channels-last input, every
+//             conv's pre-BatchNorm output y (post-activation values are
+//             recomputed on load as relu(y*scale+shift)), pooled maps, the
+//             up-convolution outputs U and the per-BatchNorm coefficients;
+//   scratch - per-call temporaries: two gradient ping-pong buffers, reduction
+//             partials and the re-laid-out weights of the layer in flight.
+// forward/backward then enqueue one fixed kernel sequence on the caller's
+// stream (no allocation, no host sync: capturable into a hipGraph).
+//
+// The decoder's cat(U, U) (crop returns U itself, hcat/unet.py:311-312,
+// 319-340) is folded into Up.conv1's weights: conv(cat(U,U), W) ==
+// conv(U, W[:, :C] + W[:, C:]) (per group), halving that layer's work; the
+// weight gradient is scattered back to both halves.
+#include "common.h"
+#include "../../include/hcunet.h"
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace hcu {
+static thread_local std::string g_err;
+void set_error(const std::string &msg) { g_err = msg; }
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+int launch_outconv_wfinalize(const float *part_oc, int R, int Co, int C, int Cs, float *dw,
+                             float *db, int accumulate, hipStream_t s);
+int launch_bn_count_increment(int64_t *const *ptrs, int n, hipStream_t s);
+}  // namespace hcu
+
+using namespace hcu;
+
+namespace {
+
+constexpr int kTargetBlocks = 1024;
+
+struct Dims {
+  int B = 0, X = 0, Y = 0, Z = 0, C = 0, Cs = 0;
+  int64_t vox() const { return (int64_t)B * X * Y * Z; }
+  size_t floats() const { return (size_t)vox() * Cs; }
+};
+
+Dims mkdims(int B, int X, int Y, int Z, int C) {
+  Dims d;
+  d.B = B;
+  d.X = X;
+  d.Y = Y;
+  d.Z = Z;
+  d.C = C;
+  d.Cs = round_up(C, 4);
+  return d;
+}
+
+struct Region {
+  size_t off = 0;
+  size_t take_floats(size_t n) {
+    const size_t o = off;
+    off = align_up(off + n * sizeof(float), 256);
+    return o;
+  }
+};
+
+struct BNLayer {
+  int C = 0, Cs = 0;
+  size_t coef_off = 0;  // saved: 6 arrays of Cs floats
+  int64_t gamma = 0, beta = 0;
+  int index = 0;
+  double count = 0;
+};
+
+struct ConvLayer {
+  int Cout = 0, Cin_g = 0, groups = 1, fold_mod = 0, E = 0, T = 0;
+  int K[3], D[3];
+  int64_t w_off = 0, b_off = 0;
+  Dims in, out;
+  GConvArgs fwd{}, dgrad{};
+  WGradArgs wg{};
+  BNLayer bn;
+  size_t y_off = 0;
+};
+
+struct ConvTLayer {
+  int Cin = 0, Cout = 0, T = 0;
+  int K[3], S[3];
+  int64_t w_off = 0, b_off = 0;
+  Dims in, out;
+  std::vector<GConvArgs> phases;
+  std::vector<int> pJ;  // 6 ints per phase: px,py,pz,Jx,Jy,Jz
+  GConvArgs dgrad{};
+  WGradArgs wg{};
+  size_t u_off = 0;
+};
+
+BNCoef coef_at(char *saved, const BNLayer &bn) {
+  float *b = reinterpret_cast<float *>(saved + bn.coef_off);
+  BNCoef c;
+  c.scale = b;
+  c.shift = b + bn.Cs;
+  c.mean = b + 2 * bn.Cs;
+  c.invstd = b + 3 * bn.Cs;
+  c.c1 = b + 4 * bn.Cs;
+  c.c0 = b + 5 * bn.Cs;
+  return c;
+}
+
+GConvArgs gconv_conv_fwd(const Dims &in, const Dims &out, const int K[3], const int D[3], int Cout) {
+  GConvArgs a{};
+  a.B = in.B;
+  a.IX = in.X; a.IY = in.Y; a.IZ = in.Z; a.ICs = in.Cs;
+  a.OX = out.X; a.OY = out.Y; a.OZ = out.Z;
+  a.SX = out.X; a.SY = out.Y; a.SZ = out.Z; a.OCs = out.Cs; a.Cout = Cout;
+  a.osx = a.osy = a.osz = 1;
+  a.KX = K[0]; a.KY = K[1]; a.KZ = K[2];
+  a.sx = a.sy = a.sz = 1;
+  a.dx = D[0]; a.dy = D[1]; a.dz = D[2];
+  return a;
+}
+
+GConvArgs gconv_conv_dgrad(const Dims &in, const Dims &out, const int K[3], const int D[3], int E) {
+  GConvArgs a{};
+  a.B = in.B;
+  a.IX = out.X; a.IY = out.Y; a.IZ = out.Z; a.ICs = out.Cs;
+  a.OX = in.X; a.OY = in.Y; a.OZ = in.Z;
+  a.SX = in.X; a.SY = in.Y; a.SZ = in.Z; a.OCs = in.Cs; a.Cout = E;
+  a.osx = a.osy = a.osz = 1;
+  a.KX = K[0]; a.KY = K[1]; a.KZ = K[2];
+  a.sx = a.sy = a.sz = 1;
+  a.dx = D[0]; a.dy = D[1]; a.dz = D[2];
+  a.px = D[0] * (K[0] - 1); a.py = D[1] * (K[1] - 1); a.pz = D[2] * (K[2] - 1);
+  return a;
+}
+
+WGradArgs wgrad_conv(const Dims &in, const Dims &out, const int K[3], const int D[3]) {
+  WGradArgs w{};
+  w.B = in.B;
+  w.AX = in.X; w.AY = in.Y; w.AZ = in.Z; w.ACs = in.Cs;
+  w.GX = out.X; w.GY = out.Y; w.GZ = out.Z; w.GCs = out.Cs;
+  w.PX = out.X; w.PY = out.Y; w.PZ = out.Z;
+  w.KX = K[0]; w.KY = K[1]; w.KZ = K[2];
+  w.asx = w.asy = w.asz = 1;
+  w.adx = D[0]; w.ady = D[1]; w.adz = D[2];
+  w.gsx = w.gsy = w.gsz = 1;
+  w.taps_rows = 1;
+  w.bias_row = 1;
+  return w;
+}
+
+int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod, int cin_total,
+               const int K[3], const int D[3], const char *name) {
+  for (int i = 0; i < 3; ++i) {
+    L.K[i] = K[i];
+    L.D[i] = D[i];
+    if (K[i] < 1 || D[i] < 1) return fail(HCU_ERR_INVALID, std::string(name) + ": bad kernel/dilation");
+  }
+  if (groups < 1 || cin_total % groups || Cout % groups)
+    return fail(HCU_ERR_INVALID, std::string(name) + ": channels must be divisible by groups");
+  L.Cout = Cout;
+  L.groups = groups;
+  L.Cin_g = cin_total / groups;
+  L.fold_mod = fold_mod;
+  L.E = std::min(fold_mod, cin_total);
+  L.T = K[0] * K[1] * K[2];
+  L.in = in;
+  const int ox = in.X - D[0] * (K[0] - 1), oy = in.Y - D[1] * (K[1] - 1), oz = in.Z - D[2] * (K[2] - 1);
+  if (ox < 1 || oy < 1 || oz < 1)
+    return fail(HCU_ERR_SHAPE, std::string(name) + ": Calculated padded input size per channel: (" +
+                                   std::to_string(in.X) + " x " + std::to_string(in.Y) + " x " +
+                                   std::to_string(in.Z) +
+                                   "). Kernel size can't be greater than actual input size");
+  L.out = mkdims(in.B, ox, oy, oz, Cout);
+  L.fwd = gconv_conv_fwd(in, L.out, K, D, Cout);
+  if (int e = plan_gconv(L.fwd, kTargetBlocks)) return e;
+  L.dgrad = gconv_conv_dgrad(in, L.out, K, D, L.E);
+  if (int e = plan_gconv(L.dgrad, kTargetBlocks)) return e;
+  L.wg = wgrad_conv(in, L.out, K, D);
+  if (int e = plan_wgrad(L.wg, kTargetBlocks)) return e;
+  L.bn.C = Cout;
+  L.bn.Cs = L.out.Cs;
+  L.bn.count = (double)L.out.vox();
+  return 0;
+}
+
+
+int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int S[3],
+                size_t &max_wprep, size_t &max_part) {
+  const int f = cur.C;
+  u.Cin = f;
+  u.Cout = o;
+  u.T = K[0] * K[1] * K[2];
+  for (int d = 0; d < 3; ++d) {
+    u.K[d] = K[d];
+    u.S[d] = S[d];
+    if (K[d] < 1 || S[d] < 1) return fail(HCU_ERR_INVALID, "ConvTranspose3d: bad kernel/stride");
+  }
+  u.in = cur;
+  const int ux = (cur.X - 1) * u.S[0] + u.K[0], uy = (cur.Y - 1) * u.S[1] + u.K[1],
+            uz = (cur.Z - 1) * u.S[2] + u.K[2];
+  u.out = mkdims(cur.B, ux, uy, uz, o);
+  u.phases.clear();
+  u.pJ.clear();
+  const int nph = u.S[0] * u.S[1] * u.S[2];
+  for (int qx = 0; qx < u.S[0]; ++qx)
+    for (int qy = 0; qy < u.S[1]; ++qy)
+      for (int qz = 0; qz < u.S[2]; ++qz) {
+        const int Jx = cdiv(u.K[0] - qx, u.S[0]), Jy = cdiv(u.K[1] - qy, u.S[1]),
+                  Jz = cdiv(u.K[2] - qz, u.S[2]);
+        if (Jx < 1 || Jy < 1 || Jz < 1)
+          return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d with kernel < stride is not supported");
+        GConvArgs a{};
+        a.B = cur.B;
+        a.IX = cur.X; a.IY = cur.Y; a.IZ = cur.Z; a.ICs = cur.Cs;
+        a.OX = cdiv(ux - qx, u.S[0]); a.OY = cdiv(uy - qy, u.S[1]); a.OZ = cdiv(uz - qz, u.S[2]);
+        a.SX = ux; a.SY = uy; a.SZ = uz; a.OCs = u.out.Cs; a.Cout = o;
+        a.osx = u.S[0]; a.osy = u.S[1]; a.osz = u.S[2];
+        a.ofx = qx; a.ofy = qy; a.ofz = qz;
+        a.KX = Jx; a.KY = Jy; a.KZ = Jz;
+        a.sx = a.sy = a.sz = 1;
+        a.dx = a.dy = a.dz = 1;
+        a.px = Jx - 1; a.py = Jy - 1; a.pz = Jz - 1;
+        if (int e = plan_gconv(a, std::max(64, kTargetBlocks / nph))) return e;
+        u.phases.push_back(a);
+        const int pj[6] = {qx, qy, qz, Jx, Jy, Jz};
+        u.pJ.insert(u.pJ.end(), pj, pj + 6);
+        max_wprep = std::max(max_wprep, (size_t)Jx * Jy * Jz * a.ICs * a.CoutW);
+      }
+  {  // dgrad: strided correlation of dU with W[ci][co][t]
+    GConvArgs a{};
+    a.B = cur.B;
+    a.IX = ux; a.IY = uy; a.IZ = uz; a.ICs = u.out.Cs;
+    a.OX = cur.X; a.OY = cur.Y; a.OZ = cur.Z;
+    a.SX = cur.X; a.SY = cur.Y; a.SZ = cur.Z; a.OCs = cur.Cs; a.Cout = f;
+    a.osx = a.osy = a.osz = 1;
+    a.KX = u.K[0]; a.KY = u.K[1]; a.KZ = u.K[2];
+    a.sx = u.S[0]; a.sy = u.S[1]; a.sz = u.S[2];
+    a.dx = a.dy = a.dz = 1;
+    if (int e = plan_gconv(a, kTargetBlocks)) return e;
+    u.dgrad = a;
+    max_wprep = std::max(max_wprep, (size_t)u.T * a.ICs * a.CoutW);
+  }
+  {  // wgrad: rows = ci, cols = (t, co)
+    WGradArgs w{};
+    w.B = cur.B;
+    w.AX = cur.X; w.AY = cur.Y; w.AZ = cur.Z; w.ACs = cur.Cs;
+    w.GX = ux; w.GY = uy; w.GZ = uz; w.GCs = u.out.Cs;
+    w.PX = cur.X; w.PY = cur.Y; w.PZ = cur.Z;
+    w.KX = u.K[0]; w.KY = u.K[1]; w.KZ = u.K[2];
+    w.asx = w.asy = w.asz = 1;
+    w.gsx = u.S[0]; w.gsy = u.S[1]; w.gsz = u.S[2];
+    w.gdx = w.gdy = w.gdz = 1;
+    w.taps_rows = 0;
+    w.bias_row = 0;
+    if (int e = plan_wgrad(w, kTargetBlocks)) return e;
+    u.wg = w;
+    max_part = std::max(max_part, wgrad_partial_floats(w));
+    max_part = std::max(max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
+  }
+  return 0;
+}
+
+}  // namespace
+
+struct hcu_unet_plan {
+  hcu_unet_spec spec;
+  int B, X, Y, Z, L;
+  Dims xin;
+  size_t xcl_off = 0;
+  std::vector<ConvLayer> dc1, dc2, uc1, uc2;
+  std::vector<Dims> pooled;
+  std::vector<size_t> pool_off;
+  std::vector<ConvTLayer> up;
+  int64_t oc_w = 0, oc_b = 0;
+  int Co = 0;
+  Dims outd;
+  int64_t n_params = 0;
+  int n_bn = 0;
+  size_t saved_bytes = 0, scratch_bytes = 0;
+  // scratch layout
+  size_t buf_off[2] = {0, 0};
+  size_t part_off = 0, wprep_off = 0;
+  size_t max_act = 0, max_part = 0, max_wprep = 0;
+};
+
+namespace {
+
+size_t prep_floats_fwd(const ConvLayer &L) { return (size_t)L.T * L.fwd.ICs * L.fwd.CoutW; }
+size_t prep_floats_dgrad(const ConvLayer &L) { return (size_t)L.T * L.dgrad.ICs * L.dgrad.CoutW; }
+
+void track_conv(hcu_unet_plan &p, const ConvLayer &L) {
+  p.max_act = std::max(p.max_act, std::max(L.in.floats(), L.out.floats()));
+  p.max_part = std::max(p.max_part, (size_t)gconv_rows(L.fwd) * L.fwd.CoutW * 2);
+  p.max_part = std::max(p.max_part, wgrad_partial_floats(L.wg));
+  p.max_part = std::max(p.max_part, (size_t)bwd_rows(L.out.vox(), L.out.Cs) * L.out.Cs * 2);
+  p.max_wprep = std::max(p.max_wprep, std::max(prep_floats_fwd(L), prep_floats_dgrad(L)));
+}
+
+int build_plan(hcu_unet_plan &p) {
+  const hcu_unet_spec &s = p.spec;
+  const int L = s.levels;
+  if (L < 2 || L > HCU_MAX_LEVELS)
+    return fail(HCU_ERR_INVALID, "The Number of Features must be at least 2");
+  for (int i = 0; i + 1 < L; ++i)
+    if (s.features[i] * 2 != s.features[i + 1])
+      return fail(HCU_ERR_INVALID, "Feature Sizes must be multiples of two from each other");
+  if (s.in_channels < 1 || s.out_channels < 1 || s.features[0] < 1)
+    return fail(HCU_ERR_INVALID, "channel counts must be positive");
+  if (p.B < 1 || p.X < 1 || p.Y < 1 || p.Z < 1) return fail(HCU_ERR_SHAPE, "empty input");
+  for (int i = 0; i < 3; ++i)
+    if (s.pool_k[i] < 1 || s.up_k[i] < 1 || s.up_s[i] < 1)
+      return fail(HCU_ERR_INVALID, "bad pool/upsample kernel");
+  p.L = L;
+  p.dc1.resize(L);
+  p.dc2.resize(L);
+  p.pooled.resize(L);
+  p.pool_off.resize(L);
+  p.up.resize(L - 1);
+  p.uc1.resize(L - 1);
+  p.uc2.resize(L - 1);
+
+  // Parameter offsets in Unet_Constructor.parameters() order (hcat/unet.py:87-123:
+  // out_conv, then down_steps[i].{conv1,conv2,batch1,batch2}, then
+  // up_steps[j].{conv1,conv2,up_conv,batch1,batch2}).
+  int64_t off = 0;
+  const int f0 = s.features[0];
+  p.Co = s.out_channels;
+  p.oc_w = off; off += (int64_t)p.Co * f0;
+  p.oc_b = off; off += p.Co;
+  const int T1 = s.k1[0] * s.k1[1] * s.k1[2], T2 = s.k2[0] * s.k2[1] * s.k2[2];
+  const int Tu = s.up_k[0] * s.up_k[1] * s.up_k[2];
+  int bn_index = 0;
+  for (int i = 0; i < L; ++i) {
+    const int cin = i == 0 ? s.in_channels : s.features[i - 1];
+    const int f = s.features[i];
+    if (cin % s.g1 || f % s.g1 || f % s.g2)
+      return fail(HCU_ERR_INVALID, "in_channels/out_channels must be divisible by groups");
+    ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
+    c1.w_off = off; off += (int64_t)f * (cin / s.g1) * T1;
+    c1.b_off = off; off += f;
+    c2.w_off = off; off += (int64_t)f * (f / s.g2) * T2;
+    c2.b_off = off; off += f;
+    c1.bn.gamma = off; off += f;
+    c1.bn.beta = off; off += f;
+    c2.bn.gamma = off; off += f;
+    c2.bn.beta = off; off += f;
+    c1.bn.index = bn_index++;
+    c2.bn.index = bn_index++;
+  }
+  for (int j = 0; j < L - 1; ++j) {
+    const int f = s.features[L - 1 - j], o = s.features[L - 2 - j];
+    if (f % s.g1 || o % s.g1 || o % s.g2)
+      return fail(HCU_ERR_INVALID, "in_channels/out_channels must be divisible by groups");
+    ConvLayer &c1 = p.uc1[j], &c2 = p.uc2[j];
+    ConvTLayer &u = p.up[j];
+    c1.w_off = off; off += (int64_t)o * (f / s.g1) * T1;
+    c1.b_off = off; off += o;
+    c2.w_off = off; off += (int64_t)o * (o / s.g2) * T2;
+    c2.b_off = off; off += o;
+    u.w_off = off; off += (int64_t)f * o * Tu;
+    u.b_off = off; off += o;
+    c1.bn.gamma = off; off += o;
+    c1.bn.beta = off; off += o;
+    c2.bn.gamma = off; off += o;
+    c2.bn.beta = off; off += o;
+    c1.bn.index = bn_index++;
+    c2.bn.index = bn_index++;
+  }
+  p.n_params = off;
+  p.n_bn = bn_index;
+
+  // Shapes, forward order.
+  Region saved;
+  p.xin = mkdims(p.B, p.X, p.Y, p.Z, s.in_channels);
+  p.xcl_off = saved.take_floats(p.xin.floats());
+  p.max_act = p.xin.floats();
+  Dims cur = p.xin;
+  for (int i = 0; i < L; ++i) {
+    const int cin = cur.C, f = s.features[i];
+    if (int e = setup_conv(p.dc1[i], cur, f, s.g1, cin, cin, s.k1, s.d1, "down conv1")) return e;
+    if (int e = setup_conv(p.dc2[i], p.dc1[i].out, f, s.g2, f, f, s.k2, s.d2, "down conv2")) return e;
+    for (ConvLayer *c : {&p.dc1[i], &p.dc2[i]}) {
+      c->y_off = saved.take_floats(c->out.floats());
+      c->bn.coef_off = saved.take_floats((size_t)6 * c->bn.Cs);
+      track_conv(p, *c);
+    }
+    cur = p.dc2[i].out;
+    if (i < L - 1) {
+      const int px = cur.X / s.pool_k[0], py = cur.Y / s.pool_k[1], pz = cur.Z / s.pool_k[2];
+      if (px < 1 || py < 1 || pz < 1)
+        return fail(HCU_ERR_SHAPE, "max_pool3d: Output size is too small");
+      p.pooled[i] = mkdims(p.B, px, py, pz, f);
+      p.pool_off[i] = saved.take_floats(p.pooled[i].floats());
+      p.max_act = std::max(p.max_act, p.pooled[i].floats());
+      cur = p.pooled[i];
+    }
+  }
+  for (int j = 0; j < L - 1; ++j) {
+    const int level = L - 2 - j;
+    const int f = s.features[L - 1 - j], o = s.features[L - 2 - j];
+    ConvTLayer &u = p.up[j];
+    if (int e = setup_convt(u, cur, o, s.up_k, s.up_s, p.max_wprep, p.max_part)) return e;
+    const Dims &skip = p.dc2[level].out;
+    if (u.out.X > skip.X || u.out.Y > skip.Y || u.out.Z > skip.Z)
+      return fail(HCU_ERR_SHAPE,
+                  "Sizes of tensors must match except in dimension 1 (upsampled " +
+                      std::to_string(u.out.X) + "x" + std::to_string(u.out.Y) + "x" +
+                      std::to_string(u.out.Z) + " exceeds skip " + std::to_string(skip.X) + "x" +
+                      std::to_string(skip.Y) + "x" + std::to_string(skip.Z) + ")");
+    u.u_off = saved.take_floats(u.out.floats());
+    p.max_act = std::max(p.max_act, u.out.floats());
+    // conv1 consumes cat(U, U): fold (cat channels 2*o, effective o)
+    if (int e = setup_conv(p.uc1[j], u.out, o, s.g1, o, f, s.k1, s.d1, "up conv1")) return e;
+    if (int e = setup_conv(p.uc2[j], p.uc1[j].out, o, s.g2, o, o, s.k2, s.d2, "up conv2")) return e;
+    for (ConvLayer *c : {&p.uc1[j], &p.uc2[j]}) {
+      c->y_off = saved.take_floats(c->out.floats());
+      c->bn.coef_off = saved.take_floats((size_t)6 * c->bn.Cs);
+      track_conv(p, *c);
+    }
+    cur = p.uc2[j].out;
+  }
+  if (p.Co > 4) return fail(HCU_ERR_UNSUPPORTED, "out_channels > 4 is not supported yet");
+  p.outd = mkdims(p.B, cur.X, cur.Y, cur.Z, p.Co);
+  {
+    const int R = outconv_bwd_rows(cur.vox(), cur.Cs);
+    p.max_part = std::max(p.max_part, (size_t)R * cur.Cs * 2 + (size_t)R * (p.Co * cur.Cs + p.Co) + 64);
+  }
+  p.saved_bytes = saved.off;
+
+  Region scratch;
+  p.buf_off[0] = scratch.take_floats(p.max_act);
+  p.buf_off[1] = scratch.take_floats(p.max_act);
+  p.part_off = scratch.take_floats(p.max_part);
+  p.wprep_off = scratch.take_floats(p.max_wprep);
+  p.scratch_bytes = scratch.off;
+  return 0;
+}
+
+struct Ctx {
+  const hcu_unet_plan &p;
+  const hcu_unet_tensors &t;
+  hipStream_t s;
+  char *sv, *sc;
+  const float *P;
+  float *G;
+  float *fptr(char *base, size_t off) const { return reinterpret_cast<float *>(base + off); }
+  float *part() const { return fptr(sc, p.part_off); }
+  float *wprep() const { return fptr(sc, p.wprep_off); }
+  float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
+};
+
+int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float *isc,
+                 const float *ish, int training) {
+  HCU_HIP(hipGetLastError());
+  if (int e = launch_prep_conv_fwd(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups, L.fold_mod,
+                                   L.T, L.fwd.ICs, L.fwd.CoutW, c.s))
+    return e;
+  GConvArgs a = L.fwd;
+  a.in = in;
+  a.in_scale = isc;
+  a.in_shift = ish;
+  a.w = c.wprep();
+  a.bias = c.P + L.b_off;
+  a.out = c.fptr(c.sv, L.y_off);
+  a.stats = training ? c.part() : nullptr;
+  if (int e = launch_gconv(a, c.s)) return e;
+  const BNCoef coef = coef_at(c.sv, L.bn);
+  return launch_bn_fwd_finalize(c.part(), gconv_rows(L.fwd), L.fwd.CoutW, L.bn.C, L.bn.Cs,
+                                L.bn.count, c.P + L.bn.gamma, c.P + L.bn.beta,
+                                c.t.bn_running_mean[L.bn.index], c.t.bn_running_var[L.bn.index],
+                                c.t.bn_num_batches_tracked[L.bn.index], c.p.spec.bn_eps,
+                                c.p.spec.bn_momentum, training, coef, c.s);
+}
+
+// Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
+int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float *asc,
+                  const float *ash, const float *dy, float *dA, int accumulate) {
+  WGradArgs w = L.wg;
+  w.A = A;
+  w.a_scale = asc;
+  w.a_shift = ash;
+  w.G = dy;
+  w.partial = c.part();
+  if (int e = launch_wgrad(w, c.s)) return e;
+  WGradFinalize f{};
+  f.partial = c.part();
+  f.dw = c.G + L.w_off;
+  f.db = c.G + L.b_off;
+  f.KB = w.KB;
+  f.Mtot = w.Mtot;
+  f.Ntot = w.Ntot;
+  f.T = L.T;
+  f.mode = 0;
+  f.Cout = L.Cout;
+  f.Cin_g = L.Cin_g;
+  f.groups = L.groups;
+  f.fold_mod = L.fold_mod;
+  f.ACs = w.ACs;
+  f.accumulate = accumulate;
+  if (int e = launch_wgrad_finalize(f, c.s)) return e;
+  if (!dA) return 0;
+  if (int e = launch_prep_conv_dgrad(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups,
+                                     L.fold_mod, L.T, L.dgrad.ICs, L.dgrad.CoutW, L.E, c.s))
+    return e;
+  GConvArgs a = L.dgrad;
+  a.in = dy;
+  a.w = c.wprep();
+  a.out = dA;
+  return launch_gconv(a, c.s);
+}
+
+// BatchNorm+ReLU backward for layer L: dbuf holds d(post-activation) on entry
+// and d(pre-BN y) on exit (unless pool_dP is given, in which case dbuf is
+// produced from the max-pool gradient).
+int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool_dP,
+                const int *pool_k, int training, int accumulate) {
+  const BNCoef coef = coef_at(c.sv, L.bn);
+  const float *y = c.fptr(c.sv, L.y_off);
+  const int64_t nvox = L.out.vox();
+  const int R = bwd_rows(nvox, L.out.Cs);
+  if (pool_dP) {
+    if (int e = launch_bn_bwd_reduce_pool(pool_dP, y, coef, dbuf, L.out.B, L.out.X, L.out.Y,
+                                          L.out.Z, L.out.Cs, pool_k[0], pool_k[1], pool_k[2],
+                                          c.part(), R, c.s))
+      return e;
+  } else {
+    if (int e = launch_bn_bwd_reduce_dense(dbuf, y, coef, nvox, L.out.Cs, c.part(), R, c.s))
+      return e;
+  }
+  if (int e = launch_bn_bwd_finalize(c.part(), R, L.bn.C, L.bn.Cs, L.bn.count, coef,
+                                     c.G + L.bn.gamma, c.G + L.bn.beta, training, accumulate, c.s))
+    return e;
+  return launch_bn_bwd_apply(dbuf, y, coef, nvox, L.out.Cs, c.s);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *hcu_last_error(void) { return g_err.c_str(); }
+int hcu_version(void) { return 100; }
+
+int hcu_unet_plan_create(const hcu_unet_spec *spec, int B, int X, int Y, int Z,
+                         hcu_unet_plan **out) {
+  if (!spec || !out) return fail(HCU_ERR_INVALID, "null argument");
+  auto *p = new hcu_unet_plan();
+  p->spec = *spec;
+  p->B = B;
+  p->X = X;
+  p->Y = Y;
+  p->Z = Z;
+  const int e = build_plan(*p);
+  if (e) {
+    delete p;
+    *out = nullptr;
+    return e;
+  }
+  *out = p;
+  return HCU_OK;
+}
+
+void hcu_unet_plan_destroy(hcu_unet_plan *plan) { delete plan; }
+
+int hcu_unet_plan_query(const hcu_unet_plan *p, int64_t *out_shape, int64_t *n_params, int *n_bn,
+                        size_t *saved_bytes, size_t *scratch_bytes) {
+  if (!p) return fail(HCU_ERR_INVALID, "null plan");
+  if (out_shape) {
+    out_shape[0] = p->B;
+    out_shape[1] = p->Co;
+    out_shape[2] = p->outd.X;
+    out_shape[3] = p->outd.Y;
+    out_shape[4] = p->outd.Z;
+  }
+  if (n_params) *n_params = p->n_params;
+  if (n_bn) *n_bn = p->n_bn;
+  if (saved_bytes) *saved_bytes = p->saved_bytes;
+  if (scratch_bytes) *scratch_bytes = p->scratch_bytes;
+  return HCU_OK;
+}
+
+int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
+                     hcu_stream_t stream) {
+  if (!plan || !t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
+    return fail(HCU_ERR_INVALID, "null argument");
+  const hcu_unet_plan &p = *plan;
+  if (training) {
+    for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
+      for (const ConvLayer &L : *v)
+        if (L.bn.count <= 1.0)
+          return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
+  }
+  Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  const hcu_unet_spec &s = p.spec;
+  float *xcl = c.fptr(c.sv, p.xcl_off);
+  if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
+  const float *src = xcl;
+  const float *ssc = nullptr, *ssh = nullptr;
+  for (int i = 0; i < p.L; ++i) {
+    const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
+    if (int e = conv_forward(c, c1, src, ssc, ssh, training)) return e;
+    const BNCoef b1 = coef_at(c.sv, c1.bn);
+    if (int e = conv_forward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, training)) return e;
+    const BNCoef b2 = coef_at(c.sv, c2.bn);
+    if (i < p.L - 1) {
+      float *pp = c.fptr(c.sv, p.pool_off[i]);
+      if (int e = launch_maxpool_fwd(c.fptr(c.sv, c2.y_off), b2.scale, b2.shift, pp, p.B,
+                                     c2.out.X, c2.out.Y, c2.out.Z, c2.out.Cs, s.pool_k[0],
+                                     s.pool_k[1], s.pool_k[2], c.s))
+        return e;
+      src = pp;
+      ssc = ssh = nullptr;
+    } else {
+      src = c.fptr(c.sv, c2.y_off);
+      ssc = b2.scale;
+      ssh = b2.shift;
+    }
+  }
+  for (int j = 0; j < p.L - 1; ++j) {
+    const ConvTLayer &u = p.up[j];
+    float *U = c.fptr(c.sv, u.u_off);
+    for (size_t ph = 0; ph < u.phases.size(); ++ph) {
+      const int *pj = &u.pJ[ph * 6];
+      GConvArgs a = u.phases[ph];
+      if (int e = launch_prep_convt_fwd(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.K[0], u.K[1],
+                                        u.K[2], u.S[0], u.S[1], u.S[2], pj[0], pj[1], pj[2],
+                                        pj[3], pj[4], pj[5], a.ICs, a.CoutW, c.s))
+        return e;
+      a.in = src;
+      a.in_scale = ssc;
+      a.in_shift = ssh;
+      a.w = c.wprep();
+      a.bias = c.P + u.b_off;
+      a.out = U;
+      a.stats = nullptr;
+      if (int e = launch_gconv(a, c.s)) return e;
+    }
+    const ConvLayer &c1 = p.uc1[j], &c2 = p.uc2[j];
+    if (int e = conv_forward(c, c1, U, nullptr, nullptr, training)) return e;
+    const BNCoef b1 = coef_at(c.sv, c1.bn);
+    if (int e = conv_forward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, training)) return e;
+    const BNCoef b2 = coef_at(c.sv, c2.bn);
+    src = c.fptr(c.sv, c2.y_off);
+    ssc = b2.scale;
+    ssh = b2.shift;
+  }
+  const ConvLayer &last = p.L > 1 ? p.uc2[p.L - 2] : p.dc2[0];
+  if (int e = launch_outconv_fwd(src, coef_at(c.sv, last.bn), c.P + p.oc_w, c.P + p.oc_b, t->out,
+                                 p.B, last.out.vox() / p.B, last.out.C, last.out.Cs, p.Co, c.s))
+    return e;
+  if (training && t->bn_num_batches_tracked)
+    if (int e = launch_bn_count_increment(t->bn_num_batches_tracked, p.n_bn, c.s)) return e;
+  return HCU_OK;
+}
+
+int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, const float *dout,
+                      float *dx, int training, int accumulate, hcu_stream_t stream) {
+  if (!plan || !t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)
+    return fail(HCU_ERR_INVALID, "null argument");
+  const hcu_unet_plan &p = *plan;
+  const hcu_unet_spec &s = p.spec;
+  Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  int cur = 0;  // index of the buffer holding the current d(pre-BN y)
+
+  // out_conv + last BatchNorm
+  const ConvLayer &last = p.uc2[p.L - 2];
+  {
+    const BNCoef coef = coef_at(c.sv, last.bn);
+    const int64_t nvox = last.out.vox();
+    const int R = outconv_bwd_rows(nvox, last.out.Cs);
+    float *part_bn = c.part();
+    float *part_oc = part_bn + (size_t)R * last.out.Cs * 2;
+    if (int e = launch_outconv_bwd(dout, c.fptr(c.sv, last.y_off), coef, c.P + p.oc_w, c.buf(cur),
+                                   p.B, nvox / p.B, last.out.C, last.out.Cs, p.Co, part_bn, part_oc,
+                                   R, c.s))
+      return e;
+    if (int e = launch_outconv_wfinalize(part_oc, R, p.Co, last.out.C, last.out.Cs, c.G + p.oc_w,
+                                         c.G + p.oc_b, accumulate, c.s))
+      return e;
+    if (int e = launch_bn_bwd_finalize(part_bn, R, last.bn.C, last.bn.Cs, last.bn.count, coef,
+                                       c.G + last.bn.gamma, c.G + last.bn.beta, training,
+                                       accumulate, c.s))
+      return e;
+    if (int e = launch_bn_bwd_apply(c.buf(cur), c.fptr(c.sv, last.y_off), coef, nvox,
+                                    last.out.Cs, c.s))
+      return e;
+  }
+  // decoder, last to first
+  for (int j = p.L - 2; j >= 0; --j) {
+    const ConvLayer &c1 = p.uc1[j], &c2 = p.uc2[j];
+    const ConvTLayer &u = p.up[j];
+    const BNCoef b1 = coef_at(c.sv, c1.bn);
+    const float *U = c.fptr(c.sv, u.u_off);
+    float *A = c.buf(cur), *Bf = c.buf(1 - cur);
+    // conv2
+    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate))
+      return e;
+    if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
+    // conv1 (folded cat)
+    if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, A, accumulate)) return e;
+    // up_conv: bias, weight, input gradients (A holds dU)
+    {
+      const int R = chansum_rows(u.out.vox(), u.out.Cs);
+      if (int e = launch_chansum(A, u.out.vox(), u.out.Cs, c.part(), R, c.s)) return e;
+      if (int e = launch_reduce_partials(c.part(), R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate, c.s))
+        return e;
+    }
+    const ConvLayer &prev = j == 0 ? p.dc2[p.L - 1] : p.uc2[j - 1];
+    const BNCoef bp = coef_at(c.sv, prev.bn);
+    {
+      WGradArgs w = u.wg;
+      w.A = c.fptr(c.sv, prev.y_off);
+      w.a_scale = bp.scale;
+      w.a_shift = bp.shift;
+      w.G = A;
+      w.partial = c.part();
+      if (int e = launch_wgrad(w, c.s)) return e;
+      WGradFinalize f{};
+      f.partial = c.part();
+      f.dw = c.G + u.w_off;
+      f.db = nullptr;
+      f.KB = w.KB;
+      f.Mtot = w.Mtot;
+      f.Ntot = w.Ntot;
+      f.T = u.T;
+      f.mode = 1;
+      f.Cin = u.Cin;
+      f.CoutT = u.Cout;
+      f.GCs = w.GCs;
+      f.accumulate = accumulate;
+      if (int e = launch_wgrad_finalize(f, c.s)) return e;
+    }
+    if (int e = launch_prep_convt_dgrad(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.T, u.dgrad.ICs,
+                                        u.dgrad.CoutW, c.s))
+      return e;
+    {
+      GConvArgs a = u.dgrad;
+      a.in = A;
+      a.w = c.wprep();
+      a.out = Bf;
+      if (int e = launch_gconv(a, c.s)) return e;
+    }
+    if (int e = bn_backward(c, prev, Bf, nullptr, nullptr, training, accumulate)) return e;
+    cur = 1 - cur;
+  }
+  // encoder, bottleneck to first
+  for (int i = p.L - 1; i >= 0; --i) {
+    const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
+    const BNCoef b1 = coef_at(c.sv, c1.bn);
+    float *A = c.buf(cur), *Bf = c.buf(1 - cur);
+    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate))
+      return e;
+    if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
+    const float *in = i == 0 ? c.fptr(c.sv, p.xcl_off) : c.fptr(c.sv, p.pool_off[i - 1]);
+    float *dIn = (i > 0 || dx) ? A : nullptr;
+    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, dIn, accumulate)) return e;
+    if (i > 0) {
+      // A = d(pooled), produce d(pre-BN y2_{i-1}) into Bf
+      if (int e = bn_backward(c, p.dc2[i - 1], Bf, A, s.pool_k, training, accumulate)) return e;
+      cur = 1 - cur;
+    } else if (dx) {
+      if (int e = launch_from_cl(A, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
+    }
+  }
+  return HCU_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Per-op entry points (channels-last), sharing the executor's layer setup.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct OpPlan {
+  ConvLayer conv;
+  ConvTLayer ct;
+  size_t max_wprep = 0, max_part = 0;
+  size_t wprep_off = 0, part_off = 0, scratch_bytes = 0;
+};
+
+int make_op(const hcu_conv_desc *d, OpPlan &op) {
+  if (!d) return fail(HCU_ERR_INVALID, "null descriptor");
+  const Dims in = mkdims(d->B, d->X, d->Y, d->Z, d->Cin);
+  if (!d->transposed) {
+    for (int i = 0; i < 3; ++i)
+      if (d->stride[i] != 1) return fail(HCU_ERR_UNSUPPORTED, "Conv3d: only stride 1 (valid) is supported");
+    if (int e = setup_conv(op.conv, in, d->Cout, d->groups, d->Cin, d->Cin, d->k, d->dil, "conv3d"))
+      return e;
+    op.max_wprep = std::max(prep_floats_fwd(op.conv), prep_floats_dgrad(op.conv));
+    op.max_part = wgrad_partial_floats(op.conv.wg);
+  } else {
+    if (d->groups != 1) return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d: groups must be 1");
+    for (int i = 0; i < 3; ++i)
+      if (d->dil[i] != 1) return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d: dilation must be 1");
+    if (int e = setup_convt(op.ct, in, d->Cout, d->k, d->stride, op.max_wprep, op.max_part)) return e;
+  }
+  Region r;
+  op.wprep_off = r.take_floats(op.max_wprep);
+  op.part_off = r.take_floats(op.max_part);
+  op.scratch_bytes = r.off;
+  return 0;
+}
+
+int check_scratch(const OpPlan &op, void *scratch, size_t bytes) {
+  if (bytes < op.scratch_bytes || (!scratch && op.scratch_bytes))
+    return fail(HCU_ERR_WORKSPACE, "scratch workspace too small: need " + std::to_string(op.scratch_bytes));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t hcu_conv_scratch_bytes(const hcu_conv_desc *d) {
+  OpPlan op;
+  if (make_op(d, op)) return 0;
+  return op.scratch_bytes;
+}
+
+int hcu_conv_out_dims(const hcu_conv_desc *d, int *out) {
+  OpPlan op;
+  if (int e = make_op(d, op)) return e;
+  const Dims &o = d->transposed ? op.ct.out : op.conv.out;
+  out[0] = o.X;
+  out[1] = o.Y;
+  out[2] = o.Z;
+  return HCU_OK;
+}
+
+int hcu_conv_fwd_cl(const hcu_conv_desc *d, const float *x, const float *w, const float *bias,
+                    float *y, void *scratch, size_t scratch_bytes, hcu_stream_t stream) {
+  OpPlan op;
+  if (int e = make_op(d, op)) return e;
+  if (int e = check_scratch(op, scratch, scratch_bytes)) return e;
+  hipStream_t s = (hipStream_t)stream;
+  float *wprep = reinterpret_cast<float *>((char *)scratch + op.wprep_off);
+  if (!d->transposed) {
+    const ConvLayer &L = op.conv;
+    if (int e = launch_prep_conv_fwd(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
+                                     L.fwd.ICs, L.fwd.CoutW, s))
+      return e;
+    GConvArgs a = L.fwd;
+    a.in = x;
+    a.w = wprep;
+    a.bias = bias;
+    a.out = y;
+    return launch_gconv(a, s);
+  }
+  const ConvTLayer &u = op.ct;
+  for (size_t ph = 0; ph < u.phases.size(); ++ph) {
+    const int *pj = &u.pJ[ph * 6];
+    GConvArgs a = u.phases[ph];
+    if (int e = launch_prep_convt_fwd(w, wprep, u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0],
+                                      u.S[1], u.S[2], pj[0], pj[1], pj[2], pj[3], pj[4], pj[5],
+                                      a.ICs, a.CoutW, s))
+      return e;
+    a.in = x;
+    a.w = wprep;
+    a.bias = bias;
+    a.out = y;
+    if (int e = launch_gconv(a, s)) return e;
+  }
+  return HCU_OK;
+}
+
+int hcu_conv_dgrad_cl(const hcu_conv_desc *d, const float *dy, const float *w, float *dx,
+                      void *scratch, size_t scratch_bytes, hcu_stream_t stream) {
+  OpPlan op;
+  if (int e = make_op(d, op)) return e;
+  if (int e = check_scratch(op, scratch, scratch_bytes)) return e;
+  hipStream_t s = (hipStream_t)stream;
+  float *wprep = reinterpret_cast<float *>((char *)scratch + op.wprep_off);
+  GConvArgs a;
+  if (!d->transposed) {
+    const ConvLayer &L = op.conv;
+    if (int e = launch_prep_conv_dgrad(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
+                                       L.dgrad.ICs, L.dgrad.CoutW, L.E, s))
+      return e;
+    a = L.dgrad;
+  } else {
+    const ConvTLayer &u = op.ct;
+    if (int e = launch_prep_convt_dgrad(w, wprep, u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW, s))
+      return e;
+    a = u.dgrad;
+  }
+  a.in = dy;
+  a.w = wprep;
+  a.out = dx;
+  return launch_gconv(a, s);
+}
+
+int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy, float *dw,
+                      float *dbias, void *scratch, size_t scratch_bytes, hcu_stream_t stream) {
+  OpPlan op;
+  if (int e = make_op(d, op)) return e;
+  if (int e = check_scratch(op, scratch, scratch_bytes)) return e;
+  hipStream_t s = (hipStream_t)stream;
+  float *part = reinterpret_cast<float *>((char *)scratch + op.part_off);
+  WGradFinalize f{};
+  WGradArgs w;
+  if (!d->transposed) {
+    const ConvLayer &L = op.conv;
+    w = L.wg;
+    f.mode = 0;
+    f.T = L.T;
+    f.Cout = L.Cout;
+    f.Cin_g = L.Cin_g;
+    f.groups = L.groups;
+    f.fold_mod = L.fold_mod;
+    f.db = dbias;
+  } else {
+    const ConvTLayer &u = op.ct;
+    w = u.wg;
+    f.mode = 1;
+    f.T = u.T;
+    f.Cin = u.Cin;
+    f.CoutT = u.Cout;
+  }
+  w.A = x;
+  w.G = dy;
+  w.partial = part;
+  if (int e = launch_wgrad(w, s)) return e;
+  f.partial = part;
+  f.dw = dw;
+  f.KB = w.KB;
+  f.Mtot = w.Mtot;
+  f.Ntot = w.Ntot;
+  f.ACs = w.ACs;
+  f.GCs = w.GCs;
+  if (int e = launch_wgrad_finalize(f, s)) return e;
+  if (d->transposed && dbias) {
+    const ConvTLayer &u = op.ct;
+    const int R = chansum_rows(u.out.vox(), u.out.Cs);
+    if (int e = launch_chansum(dy, u.out.vox(), u.out.Cs, part, R, s)) return e;
+    if (int e = launch_reduce_partials(part, R, u.out.Cs, u.Cout, dbias, 0, s)) return e;
+  }
+  return HCU_OK;
+}
+
+int hcu_maxpool_fwd_cl(int B, int C, int X, int Y, int Z, const int *k, const float *x, float *y,
+                       hcu_stream_t stream) {
+  if (!k || k[0] < 1 || k[1] < 1 || k[2] < 1) return fail(HCU_ERR_INVALID, "bad pool kernel");
+  if (X / k[0] < 1 || Y / k[1] < 1 || Z / k[2] < 1)
+    return fail(HCU_ERR_SHAPE, "max_pool3d: Output size is too small");
+  return launch_maxpool_fwd(x, nullptr, nullptr, y, B, X, Y, Z, round_up(C, 4), k[0], k[1], k[2],
+                            (hipStream_t)stream);
+}
+
+size_t hcu_loss_pixel_scratch_bytes(int64_t n_pred) {
+  return align_up((size_t)loss_rows(n_pred) * sizeof(float), 256);
+}
+
+int hcu_loss_pixel_fwd(const float *pred, int B, int C, int PX, int PY, int PZ, const void *mask,
+                       int mask_dtype, const void *pwl, int pwl_dtype, int MX, int MY, int MZ,
+                       float *loss, float *dpred, void *scratch, size_t scratch_bytes,
+                       hcu_stream_t stream) {
+  if (!pred || !mask || !loss || !scratch) return fail(HCU_ERR_INVALID, "null argument");
+  if (MX < PX || MY < PY || MZ < PZ)
+    return fail(HCU_ERR_SHAPE, "mask/pwl smaller than the prediction");
+  if (mask_dtype < 0 || mask_dtype > 2 || pwl_dtype < 0 || pwl_dtype > 1)
+    return fail(HCU_ERR_INVALID, "unsupported mask/pwl dtype");
+  const int64_t n = (int64_t)B * C * PX * PY * PZ;
+  if (scratch_bytes < hcu_loss_pixel_scratch_bytes(n))
+    return fail(HCU_ERR_WORKSPACE, "loss scratch too small");
+  return launch_loss_pixel(pred, B, C, PX, PY, PZ, mask, mask_dtype, pwl, pwl_dtype, MX, MY, MZ,
+                           loss, dpred, (float *)scratch, loss_rows(n), (hipStream_t)stream);
+}
+
+int hcu_scale_by_device_scalar(const float *src, const float *scale, float *dst, int64_t n,
+                               hcu_stream_t stream) {
+  return launch_scale(src, scale, dst, n, (hipStream_t)stream);
+}
+
+int hcu_adam_step(float *p, const float *g, float *m, float *v, int64_t n, float lr, float beta1,
+                  float beta2, float eps, float weight_decay, int64_t step, float grad_scale,
+                  hcu_stream_t stream) {
+  return launch_adam(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
+                     (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,339 @@
+// Weight gradient of Conv3d / ConvTranspose3d on fp32 MFMA.
+//
+// dW is a GEMM whose reduction dimension is the voxel grid (millions of
+// voxels) and whose M x N extent is tiny (taps*Cin x Cout).  Each workgroup
+// owns a (row chunk, col chunk) of dW and a strided subset of the voxel tiles;
+// it stages the activation halo (BatchNorm+ReLU applied on load) and the
+// gradient tile in LDS, the four waves split the voxel k-steps, and the
+// per-wave accumulators are summed through LDS in a fixed order and written as
+// one fp32 partial slab per workgroup.  wgrad_finalize sums the slabs in fp64
+// in a fixed order (bitwise reproducible, no atomics) and scatters them into
+// the PyTorch weight layout, undoing the cat(U,U) weight fold
+// (hcat/unet.py:310-313) and the grouped-conv block diagonal.
+#include "common.h"
+#include <algorithm>
+
+namespace hcu {
+
+template <int NS, int MSMAX>
+__global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kb = blockIdx.x, mc = blockIdx.y, nc = blockIdx.z;
+  const int T = a.KX * a.KY * a.KZ;
+  const int CKA = a.CKA, CKG = a.CKG;
+  const int ci0 = mc * CKA, co0 = nc * CKG;
+  const int PA = a.PA, PG = a.PG;
+  float *alds = smem;
+  float *glds = smem + CKA * PA;
+  const int HAZ = a.HAZ, HAYZ = a.HAY * a.HAZ, HAV = a.HAX * HAYZ;
+  const int HGZ = a.HGZ, HGYZ = a.HGY * a.HGZ, HGV = a.HGX * HGYZ;
+  const int MS = a.MS;
+
+  int aoff[MSMAX];
+#pragma unroll
+  for (int ms = 0; ms < MSMAX; ++ms) {
+    const int lr = ms * 16 + (lane & 15);
+    int off = -2;
+    if (a.taps_rows) {
+      const int ta = lr / CKA, c = lr % CKA;
+      if (ta < T) {
+        if (ci0 + c < a.ACs) {
+          const int kz = ta % a.KZ, q = ta / a.KZ, ky = q % a.KY, kx = q / a.KY;
+          off = c * PA + kx * a.adx * HAYZ + ky * a.ady * HAZ + kz * a.adz;
+        }
+      } else if (a.bias_row && mc == 0 && lr == T * CKA) {
+        off = -1;
+      }
+    } else {
+      if (lr < CKA && ci0 + lr < a.ACs) off = lr * PA;
+    }
+    aoff[ms] = off;
+  }
+  int goff[NS];
+#pragma unroll
+  for (int ns = 0; ns < NS; ++ns) {
+    const int lc = ns * 16 + (lane & 15);
+    int off = -2;
+    if (a.taps_rows) {
+      if (lc < CKG && co0 + lc < a.GCs) off = lc * PG;
+    } else {
+      const int tg = lc / CKG, o = lc % CKG;
+      if (tg < T && co0 + o < a.GCs) {
+        const int kz = tg % a.KZ, q = tg / a.KZ, ky = q % a.KY, kx = q / a.KY;
+        off = o * PG + kx * a.gdx * HGYZ + ky * a.gdy * HGZ + kz * a.gdz;
+      }
+    }
+    goff[ns] = off;
+  }
+
+  floatx4 acc[MSMAX][NS];
+#pragma unroll
+  for (int ms = 0; ms < MSMAX; ++ms)
+#pragma unroll
+    for (int ns = 0; ns < NS; ++ns) acc[ms][ns] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int PT = a.TX * a.TY * a.TZ;
+  const int nks = (PT + 3) >> 2;
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int CA4 = CKA / 4, CG4 = CKG / 4;
+
+  for (int tt = kb; tt < total; tt += a.KB) {
+    const int b = tt / ntiles;
+    int tile = tt % ntiles;
+    const int tzi = tile % a.ntz;
+    tile /= a.ntz;
+    const int tyi = tile % a.nty, txi = tile / a.nty;
+    const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    __syncthreads();
+    {  // stage A halo
+      const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
+      for (int idx = tid; idx < HAV * CA4; idx += 256) {
+        const int c4 = idx % CA4, v = idx / CA4;
+        const int hz = v % HAZ, q = v / HAZ, hy = q % a.HAY, hx = q / a.HAY;
+        const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+        const int c = ci0 + c4 * 4;
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY &&
+            (unsigned)gz < (unsigned)a.AZ && c < a.ACs) {
+          val = *reinterpret_cast<const float4 *>(
+              a.A + ((((size_t)b * a.AX + gx) * a.AY + gy) * a.AZ + gz) * a.ACs + c);
+          if (a.a_scale) {
+            const float4 sc = *reinterpret_cast<const float4 *>(a.a_scale + c);
+            const float4 sh = *reinterpret_cast<const float4 *>(a.a_shift + c);
+            val.x = fmaxf(fmaf(val.x, sc.x, sh.x), 0.f);
+            val.y = fmaxf(fmaf(val.y, sc.y, sh.y), 0.f);
+            val.z = fmaxf(fmaf(val.z, sc.z, sh.z), 0.f);
+            val.w = fmaxf(fmaf(val.w, sc.w, sh.w), 0.f);
+          }
+        }
+        float *dst = alds + (c4 * 4) * PA + v;
+        dst[0] = val.x;
+        dst[PA] = val.y;
+        dst[2 * PA] = val.z;
+        dst[3 * PA] = val.w;
+      }
+    }
+    {  // stage G halo
+      const int gx0 = px0 * a.gsx - a.gpx, gy0 = py0 * a.gsy - a.gpy, gz0 = pz0 * a.gsz - a.gpz;
+      for (int idx = tid; idx < HGV * CG4; idx += 256) {
+        const int c4 = idx % CG4, v = idx / CG4;
+        const int hz = v % HGZ, q = v / HGZ, hy = q % a.HGY, hx = q / a.HGY;
+        const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+        const int c = co0 + c4 * 4;
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        if ((unsigned)gx < (unsigned)a.GX && (unsigned)gy < (unsigned)a.GY &&
+            (unsigned)gz < (unsigned)a.GZ && c < a.GCs) {
+          val = *reinterpret_cast<const float4 *>(
+              a.G + ((((size_t)b * a.GX + gx) * a.GY + gy) * a.GZ + gz) * a.GCs + c);
+        }
+        float *dst = glds + (c4 * 4) * PG + v;
+        dst[0] = val.x;
+        dst[PG] = val.y;
+        dst[2 * PG] = val.z;
+        dst[3 * PG] = val.w;
+      }
+    }
+    __syncthreads();
+    for (int ks = wave; ks < nks; ks += 4) {
+      const int p = ks * 4 + (lane >> 4);
+      const bool pv = p < PT;
+      const int pp = pv ? p : 0;
+      const int lz = pp % a.TZ, q = pp / a.TZ, ly = q % a.TY, lx = q / a.TY;
+      const int ah = lx * a.asx * HAYZ + ly * a.asy * HAZ + lz * a.asz;
+      const int gh = lx * a.gsx * HGYZ + ly * a.gsy * HGZ + lz * a.gsz;
+      float bv[NS];
+#pragma unroll
+      for (int ns = 0; ns < NS; ++ns) bv[ns] = (pv && goff[ns] >= 0) ? glds[goff[ns] + gh] : 0.f;
+#pragma unroll
+      for (int ms = 0; ms < MSMAX; ++ms) {
+        if (ms < MS) {
+          const int o = aoff[ms];
+          float av = (o >= 0) ? alds[(o >= 0 ? o : 0) + ah] : (o == -1 ? 1.f : 0.f);
+          av = pv ? av : 0.f;
+#pragma unroll
+          for (int ns = 0; ns < NS; ++ns)
+            acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[ns], acc[ms][ns], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- cross-wave reduction in a fixed order, then one partial slab write
+  __syncthreads();
+  float *red = smem;  // [MS*NS][64][4]
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int ms = 0; ms < MSMAX; ++ms) {
+        if (ms < MS) {
+#pragma unroll
+          for (int ns = 0; ns < NS; ++ns) {
+            float *dst = red + ((ms * NS + ns) * 64 + lane) * 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[r] = (w == 0) ? acc[ms][ns][r] : dst[r] + acc[ms][ns][r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int nel = MS * NS * 256;
+  for (int idx = tid; idx < nel; idx += 256) {
+    const int r = idx & 3, ln = (idx >> 2) & 63, ti = idx >> 8;
+    const int ms = ti / NS, ns = ti % NS;
+    const int lr = ms * 16 + (ln >> 4) * 4 + r;
+    const int lc = ns * 16 + (ln & 15);
+    int grow = -1, gcol = -1;
+    if (a.taps_rows) {
+      if (lr < T * CKA) {
+        const int ci = ci0 + lr % CKA;
+        if (ci < a.ACs) grow = (lr / CKA) * a.ACs + ci;
+      } else if (a.bias_row && mc == 0 && lr == T * CKA) {
+        grow = T * a.ACs;
+      }
+      if (lc < CKG && co0 + lc < a.GCs) gcol = co0 + lc;
+    } else {
+      if (lr < CKA && ci0 + lr < a.ACs) grow = ci0 + lr;
+      const int tg = lc / CKG, o = lc % CKG;
+      if (tg < T && co0 + o < a.GCs) gcol = tg * a.GCs + co0 + o;
+    }
+    if (grow >= 0 && gcol >= 0)
+      a.partial[((size_t)kb * a.Mtot + grow) * a.Ntot + gcol] = red[idx];
+  }
+}
+
+int plan_wgrad(WGradArgs &a, int target_blocks) {
+  const int T = a.KX * a.KY * a.KZ;
+  if (a.ACs % 4 || a.GCs % 4) return fail(1, "wgrad: channel strides must be multiples of 4");
+  if (a.PX <= 0 || a.PY <= 0 || a.PZ <= 0) return fail(2, "wgrad: empty grid");
+  const int nss[3] = {4, 2, 1};
+  a.NS = 0;
+  for (int i = 0; i < 3; ++i) {
+    const int NS = nss[i], MSMAX = 16 / NS;
+    if (a.taps_rows) {
+      if (NS > 1 && (NS / 2) * 16 >= a.GCs) continue;  // do not waste columns
+      int cka = ((MSMAX * 16 - (a.bias_row ? 1 : 0)) / T) / 4 * 4;
+      cka = std::min(cka, a.ACs);
+      if (cka < 4) continue;
+      a.CKA = cka;
+      a.CKG = std::min(a.GCs, NS * 16);
+      a.mloc = T * cka + (a.bias_row ? 1 : 0);
+      a.nloc = a.CKG;
+    } else {
+      int ckg = (NS * 16 / T) / 4 * 4;
+      ckg = std::min(ckg, a.GCs);
+      if (ckg < 4) continue;
+      a.CKG = ckg;
+      a.CKA = std::min(a.ACs, MSMAX * 16);
+      a.mloc = a.CKA;
+      a.nloc = T * ckg;
+    }
+    a.NS = NS;
+    a.MS = cdiv(a.mloc, 16);
+    break;
+  }
+  if (!a.NS) return fail(4, "wgrad: kernel too large for the tile");
+  a.mchunks = cdiv(a.ACs, a.CKA);
+  a.nchunks = cdiv(a.GCs, a.CKG);
+  a.Mtot = a.taps_rows ? T * a.ACs + (a.bias_row ? 1 : 0) : a.ACs;
+  a.Ntot = a.taps_rows ? a.GCs : T * a.GCs;
+  const int ntz = cdiv(a.PZ, 16);
+  a.TZ = cdiv(a.PZ, ntz);
+  int txy = std::max(1, 256 / a.TZ);
+  for (;;) {
+    int TX = 1;
+    while ((TX + 1) * (TX + 1) <= txy) ++TX;
+    int TY = std::max(1, txy / TX);
+    TX = std::min(TX, a.PX);
+    TY = std::min(TY, a.PY);
+    a.TX = TX;
+    a.TY = TY;
+    a.HAX = (TX - 1) * a.asx + (a.KX - 1) * a.adx + 1;
+    a.HAY = (TY - 1) * a.asy + (a.KY - 1) * a.ady + 1;
+    a.HAZ = (a.TZ - 1) * a.asz + (a.KZ - 1) * a.adz + 1;
+    a.HGX = (TX - 1) * a.gsx + (a.KX - 1) * a.gdx + 1;
+    a.HGY = (TY - 1) * a.gsy + (a.KY - 1) * a.gdy + 1;
+    a.HGZ = (a.TZ - 1) * a.gsz + (a.KZ - 1) * a.gdz + 1;
+    const int HAV = a.HAX * a.HAY * a.HAZ, HGV = a.HGX * a.HGY * a.HGZ;
+    a.PA = HAV + ((1 - HAV % 32) + 32) % 32;
+    a.PG = HGV + ((1 - HGV % 32) + 32) % 32;
+    long lds = ((long)a.CKA * a.PA + (long)a.CKG * a.PG) * 4;
+    const long red = (long)a.MS * a.NS * 256 * 4;
+    if (lds < red) lds = red;
+    if (lds <= 65536 || txy == 1) {
+      a.lds_bytes = (int)lds;
+      break;
+    }
+    txy = std::max(1, txy / 2);
+  }
+  if (a.lds_bytes > 65536) return fail(4, "wgrad: tile does not fit LDS");
+  a.ntx = cdiv(a.PX, a.TX);
+  a.nty = cdiv(a.PY, a.TY);
+  a.ntz = ntz;
+  const long total = (long)a.B * a.ntx * a.nty * a.ntz;
+  const long per = (long)a.mchunks * a.nchunks;
+  long kb = std::max(1L, (long)target_blocks / per);
+  kb = std::min(kb, total);
+  a.KB = (int)kb;
+  return 0;
+}
+
+int launch_wgrad(const WGradArgs &a, hipStream_t s) {
+  const dim3 grid(a.KB, a.mchunks, a.nchunks);
+  if (a.NS == 4) {
+    hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, dim3(256), a.lds_bytes, s, a);
+  } else if (a.NS == 2) {
+    hipLaunchKernelGGL((wgrad_kernel<2, 8>), grid, dim3(256), a.lds_bytes, s, a);
+  } else {
+    hipLaunchKernelGGL((wgrad_kernel<1, 16>), grid, dim3(256), a.lds_bytes, s, a);
+  }
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize f) {
+  const int64_t n = (int64_t)f.Mtot * f.Ntot;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n;
+       idx += (int64_t)gridDim.x * 256) {
+    double s = 0.0;
+    for (int k = 0; k < f.KB; ++k) s += (double)f.partial[(size_t)k * n + idx];
+    const float v = (float)s;
+    const int grow = (int)(idx / f.Ntot), gcol = (int)(idx % f.Ntot);
+    if (f.mode == 0) {
+      const int o = gcol;
+      if (o >= f.Cout) continue;
+      if (grow == f.T * f.ACs) {
+        if (f.db) f.db[o] = f.accumulate ? f.db[o] + v : v;
+        continue;
+      }
+      const int t = grow / f.ACs, e = grow % f.ACs;
+      const int g = o / (f.Cout / f.groups);
+      const int cin_total = f.groups * f.Cin_g;
+      for (int cp = e; cp < cin_total; cp += f.fold_mod) {
+        const int c = cp - g * f.Cin_g;
+        if (c >= 0 && c < f.Cin_g) {
+          float *dst = f.dw + ((size_t)o * f.Cin_g + c) * f.T + t;
+          *dst = f.accumulate ? *dst + v : v;
+        }
+      }
+    } else {
+      const int ci = grow;
+      const int t = gcol / f.GCs, co = gcol % f.GCs;
+      if (ci >= f.Cin || co >= f.CoutT) continue;
+      float *dst = f.dw + ((size_t)ci * f.CoutT + co) * f.T + t;
+      *dst = f.accumulate ? *dst + v : v;
+    }
+  }
+}
+
+int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s) {
+  const int64_t n = (int64_t)f.Mtot * f.Ntot;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f);
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu

@@ -1,0 +1,118 @@
+"""Adam for the U-Net training step (torch.optim.Adam semantics, one launch).
+
+Same constructor and update rule as torch.optim.Adam(params, lr=1e-3) used by
+the reference training pattern (tests/r_unet_test.py:24,56); amsgrad and
+maximize are not on the path.  When a param group's parameters and gradients
+are consecutive views of one flat buffer (what Unet_Constructor sets up), the
+whole group is updated by a single hcu_adam_step launch; otherwise each
+tensor gets its own launch.  Optimizer state keeps torch's per-parameter
+layout ('step', 'exp_avg', 'exp_avg_sq'), so state_dict() is compatible.
+"""
+import torch
+
+from . import _lib
+
+
+def _flat_run(tensors):
+    """(base tensor of the run, total numel) if `tensors` are consecutive fp32
+    views of one storage, else None."""
+    if not tensors:
+        return None
+    t0 = tensors[0]
+    base = t0.data_ptr()
+    off = 0
+    for t in tensors:
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.data_ptr() != base + 4 * off:
+            return None
+        off += t.numel()
+    return t0, off
+
+
+class Adam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
+                 amsgrad=False):
+        if not 0.0 <= lr:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if not 0.0 <= eps:
+            raise ValueError(f"Invalid epsilon value: {eps}")
+        if not 0.0 <= betas[0] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 0: {betas[0]}")
+        if not 0.0 <= betas[1] < 1.0:
+            raise ValueError(f"Invalid beta parameter at index 1: {betas[1]}")
+        if not 0.0 <= weight_decay:
+            raise ValueError(f"Invalid weight_decay value: {weight_decay}")
+        if amsgrad:
+            raise NotImplementedError('amsgrad is not on the accelerated path')
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                      amsgrad=False))
+
+    def _ensure_state(self, ps, flat):
+        states = [self.state[p] for p in ps]
+        if all('exp_avg' in s for s in states):
+            return
+        dev = ps[0].device
+        if flat:
+            n = sum(p.numel() for p in ps)
+            M = torch.zeros(n, dtype=torch.float32, device=dev)
+            V = torch.zeros(n, dtype=torch.float32, device=dev)
+            off = 0
+            for p, s in zip(ps, states):
+                k = p.numel()
+                s['step'] = torch.tensor(0.0)
+                s['exp_avg'] = M[off:off + k].view_as(p)
+                s['exp_avg_sq'] = V[off:off + k].view_as(p)
+                off += k
+        else:
+            for p, s in zip(ps, states):
+                if 'exp_avg' not in s:
+                    s['step'] = torch.tensor(0.0)
+                    s['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    s['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        L = _lib.lib()
+        for group in self.param_groups:
+            ps = [p for p in group['params'] if p.grad is not None]
+            if not ps:
+                continue
+            for p in ps:
+                _lib.require_device(p, 'Adam parameter')
+                if p.grad.is_sparse:
+                    raise RuntimeError('Adam does not support sparse gradients')
+            b1, b2 = group['betas']
+            prun = _flat_run(ps)
+            grun = _flat_run([p.grad for p in ps]) if prun else None
+            flat = prun is not None and grun is not None
+            self._ensure_state(ps, flat)
+            states = [self.state[p] for p in ps]
+            if flat:
+                mrun = _flat_run([s['exp_avg'] for s in states])
+                vrun = _flat_run([s['exp_avg_sq'] for s in states])
+                steps = {float(s['step']) for s in states}
+                flat = mrun is not None and vrun is not None and len(steps) == 1
+            stream = _lib.stream_handle(ps[0].device)
+            if flat:
+                step = int(float(states[0]['step'])) + 1
+                for s in states:
+                    s['step'].fill_(step)
+                _lib.check(L.hcu_adam_step(
+                    _lib.ptr(prun[0]), _lib.ptr(grun[0]), _lib.ptr(mrun[0]), _lib.ptr(vrun[0]),
+                    prun[1], group['lr'], b1, b2, group['eps'], group['weight_decay'], step, 1.0,
+                    stream), 'Adam.step')
+            else:
+                for p, s in zip(ps, states):
+                    g = p.grad
+                    if not (p.is_contiguous() and g.is_contiguous()
+                            and p.dtype == torch.float32 and g.dtype == torch.float32):
+                        raise RuntimeError('hcunet_amd.optim.Adam: contiguous fp32 tensors required')
+                    s['step'] += 1
+                    _lib.check(L.hcu_adam_step(
+                        _lib.ptr(p), _lib.ptr(g), _lib.ptr(s['exp_avg']), _lib.ptr(s['exp_avg_sq']),
+                        p.numel(), group['lr'], b1, b2, group['eps'], group['weight_decay'],
+                        int(float(s['step'])), 1.0, stream), 'Adam.step')
+        return loss

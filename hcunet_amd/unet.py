@@ -1,0 +1,517 @@
+"""Drop-in hcat.unet.Unet_Constructor whose arithmetic runs in libhcunet.so.
+
+Interface parity with the reference (hcat/unet.py):
+  * constructor signature, kwarg normalisation and errors (:16-71),
+  * module tree and registration order, hence state_dict keys and the exact
+    seeded initialisation (:87-123; nn.Conv3d / nn.BatchNorm3d /
+    nn.ConvTranspose3d are used as parameter containers so torch's default
+    init consumes the RNG in the reference's order),
+  * forward(x) (:125-143), save(filename, hyperparameters) (:145-165),
+    load(filename, to_cuda) (:167-196), evaluate(image) (:198-233).
+
+Compute: forward/backward of the whole network are ONE autograd node whose
+forward and backward are single calls into the native executor
+(hcu_unet_forward / hcu_unet_backward), which enqueue the HIP kernels on the
+current stream.  Parameters live in one flat fp32 buffer (each nn.Parameter is
+a view of it) and gradients are written into one flat buffer whose views are
+attached as .grad, so the optimizer step and the data-parallel all-reduce are
+single launches over contiguous memory.
+"""
+import ctypes
+import glob
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+# ---------------------------------------------------------------------------
+class Unet_Constructor(nn.Module):
+    def __init__(self,
+                 image_dimensions=2,
+                 in_channels=3,
+                 out_channels=2,
+                 feature_sizes=[32, 64, 128, 256, 512, 1024],
+                 kernel=(3, 3),
+                 upsample_kernel=(2, 2),
+                 max_pool_kernel=(2, 2),
+                 upsample_stride=2,
+                 dilation=1,
+                 groups=1,
+                 ):
+        """Generic symmetric U-Net builder (same contract as hcat/unet.py:16-123).
+
+        Dict-valued kernel/dilation/groups select per-step values with keys
+        'conv1' and 'conv2'; a tuple/int applies to both steps.
+        """
+        super().__init__()
+        if image_dimensions == 2:
+            conv_functions = (nn.Conv2d, nn.ConvTranspose2d, nn.MaxPool2d, nn.BatchNorm2d)
+        elif image_dimensions == 3:
+            conv_functions = (nn.Conv3d, nn.ConvTranspose3d, nn.MaxPool3d, nn.BatchNorm3d)
+        else:
+            raise ValueError(f'Does not support {image_dimensions} dimensional images')
+
+        if type(kernel) is tuple:
+            kernel = {'conv1': kernel, 'conv2': kernel}
+        if type(dilation) is int or type(dilation) is tuple:
+            dilation = {'conv1': dilation, 'conv2': dilation}
+        if type(groups) is int or type(groups) is tuple:
+            groups = {'conv1': groups, 'conv2': groups}
+
+        if len(feature_sizes) < 2:
+            raise ValueError(f'The Number of Features must be at least 2, not {len(feature_sizes)}')
+        for i, f in enumerate(feature_sizes[0:-1:1]):
+            assert f * 2 == feature_sizes[i + 1], \
+                f'Feature Sizes must be multiples of two from each other: {f} != {feature_sizes[i - 1]}*2'
+
+        self.model_specification = {
+            'image_dimensions': image_dimensions,
+            'in_channels': in_channels,
+            'out_channels': out_channels,
+            'feature_sizes': feature_sizes,
+            'kernel': kernel,
+            'upsample_kernel': upsample_kernel,
+            'max_pool_kernel': max_pool_kernel,
+            'upsample_stride': upsample_stride,
+            'dilation': dilation,
+            'groups': groups,
+        }
+
+        # Creation order decides the RNG stream of the default init: all Down
+        # blocks, then all Up blocks, then out_conv (hcat/unet.py:87-120).
+        down = [Down(conv_functions, in_channels=in_channels, out_channels=feature_sizes[0],
+                     kernel=kernel, dilation=dilation, groups=groups)]
+        for i in range(1, len(feature_sizes)):
+            down.append(Down(conv_functions, in_channels=feature_sizes[i - 1],
+                             out_channels=feature_sizes[i], kernel=kernel,
+                             dilation=dilation, groups=groups))
+        up = []
+        for i, f in enumerate(feature_sizes[:0:-1]):
+            up.append(Up(conv_functions, in_channels=f, out_channels=feature_sizes[-2 - i],
+                         kernel=kernel, upsample_kernel=upsample_kernel,
+                         upsample_stride=upsample_stride, dilation=dilation, groups=groups))
+        # Registration order (state_dict / parameters()): out_conv first.
+        self.out_conv = conv_functions[0](feature_sizes[0], out_channels, 1)
+        self.down_steps = nn.ModuleList(down)
+        self.up_steps = nn.ModuleList(up)
+        self.max_pool = conv_functions[2](max_pool_kernel)
+        self._engine = None
+
+    # -- nn.Module plumbing ------------------------------------------------
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._engine = None  # parameters were re-materialised: re-flatten lazily
+        return out
+
+    def engine(self):
+        if self._engine is None:
+            self._engine = _Engine(self)
+        return self._engine
+
+    def forward(self, x):
+        if not isinstance(x, torch.Tensor):
+            raise TypeError(f'Expected input of type torch.Tensor, not {type(x)}')
+        _lib.require_device(x, 'Unet_Constructor input')
+        eng = self.engine()
+        eng.check_input(x)
+        params = eng.params_ready()
+        return _UnetFunction.apply(x, eng, *params)
+
+    # -- checkpointing (hcat/unet.py:145-196) --------------------------------
+    def save(self, filename, hyperparameters=None):
+        model = {'state_dict': self.state_dict(),
+                 'model_specifications': self.model_specification,
+                 'hyperparameters': hyperparameters}
+        python_files = {}
+        files = glob.glob('./**/*.py', recursive=True) + glob.glob('./**/*.ipynb', recursive=True)
+        for f in files:
+            with open(f, 'r') as fh:
+                python_files[f] = fh.read()
+        model['python_files'] = python_files
+        model['tree_structure'] = glob.glob('**/*', recursive=True)
+        torch.save(model, filename)
+        return None
+
+    def load(self, filename, to_cuda=True):
+        device = 'cuda:0' if (torch.cuda.is_available() and to_cuda) else 'cpu'
+        # A .unet checkpoint is a dict of tensors, builtins and strings: the
+        # weights-only unpickler loads it without executing code from the file.
+        model = torch.load(filename, map_location=device, weights_only=True)
+        spec = model['model_specifications']
+        self.__init__(
+            image_dimensions=spec['image_dimensions'],
+            in_channels=spec['in_channels'],
+            out_channels=spec['out_channels'],
+            feature_sizes=spec['feature_sizes'],
+            kernel=spec['kernel'],
+            upsample_kernel=spec['upsample_kernel'],
+            max_pool_kernel=spec['max_pool_kernel'],
+            upsample_stride=spec['upsample_stride'],
+            dilation=spec['dilation'],
+            groups=spec['groups'],
+        )
+        self.load_state_dict(model['state_dict'])
+        self.eval()
+        try:
+            return model['hyperparameters']
+        except KeyError:
+            return None
+
+    def evaluate(self, image: torch.Tensor):
+        """Input checks of hcat/unet.py:198-203.  The reference body never fills
+        or returns its mask (tiled inference is hcat.segment's job), so this
+        returns None like the reference."""
+        if not isinstance(image, torch.Tensor):
+            raise ValueError(f'Expected image type of torch.Tensor, not {type(image)}')
+        if image.shape[1] != self.model_specification['in_channels']:
+            raise ImportError(
+                f'Image expected to have {self.model_specification["in_channels"]} not {image.shape[1]}')
+        self.eval()
+        return None
+
+
+class Down(nn.Module):
+    """Parameter container of one encoder block (hcat/unet.py:236-266)."""
+
+    def __init__(self, conv_functions: tuple, in_channels: int, out_channels: int,
+                 kernel: dict, dilation: dict, groups: dict):
+        super().__init__()
+        self.conv1 = conv_functions[0](in_channels, out_channels, kernel['conv1'],
+                                       dilation=dilation['conv1'], groups=groups['conv1'],
+                                       padding=0)
+        self.conv2 = conv_functions[0](out_channels, out_channels, kernel['conv2'],
+                                       dilation=dilation['conv2'], groups=groups['conv2'],
+                                       padding=0)
+        self.batch1 = conv_functions[3](out_channels)
+        self.batch2 = conv_functions[3](out_channels)
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, x):
+        raise NotImplementedError(
+            'Down blocks run inside Unet_Constructor.forward (one fused native call)')
+
+
+class Up(nn.Module):
+    """Parameter container of one decoder block (hcat/unet.py:269-315)."""
+
+    def __init__(self, conv_functions: tuple, in_channels: int, out_channels: int,
+                 kernel: dict, upsample_kernel: tuple, upsample_stride: int,
+                 dilation: dict, groups: dict):
+        super().__init__()
+        self.conv1 = conv_functions[0](in_channels, out_channels, kernel['conv1'],
+                                       dilation=dilation['conv1'], groups=groups['conv1'],
+                                       padding=0)
+        self.conv2 = conv_functions[0](out_channels, out_channels, kernel['conv2'],
+                                       dilation=dilation['conv2'], groups=groups['conv2'],
+                                       padding=0)
+        if conv_functions[1] == torch.nn.modules.conv.ConvTranspose3d:
+            self.up_conv = conv_functions[1](in_channels, out_channels, upsample_kernel,
+                                             stride=upsample_stride, padding=0)
+            self.lin_up = False
+        elif conv_functions[1] == torch.nn.Upsample:
+            self.lin_up = True
+        else:
+            # hcat/unet.py:302-303: only ConvTranspose3d is accepted, so every
+            # 2D network fails here, as it does in the reference.
+            raise RuntimeError('unsupported upsampling function', conv_functions[1])
+        self.batch1 = conv_functions[3](out_channels)
+        self.batch2 = conv_functions[3](out_channels)
+        self.relu = nn.ReLU(inplace=True)
+
+    def forward(self, x, y):
+        raise NotImplementedError(
+            'Up blocks run inside Unet_Constructor.forward (one fused native call)')
+
+
+def crop(x, y):
+    """hcat/unet.py:318-340: x sliced to y's spatial extent (views only)."""
+    assert x.shape[1] == y.shape[1], \
+        f'Inputs do not have same number of feature dimmensions: {x.shape} | {y.shape}'
+    if x.dim() == 4:
+        return x[:, :, 0:y.shape[2]:1, 0:y.shape[3]:1]
+    if x.dim() == 5:
+        return x[:, :, 0:y.shape[2]:1, 0:y.shape[3]:1, 0:y.shape[4]:1]
+    return torch.empty(0)
+
+
+# ---------------------------------------------------------------------------
+def _triple(v):
+    if isinstance(v, int):
+        return (v, v, v)
+    v = tuple(v)
+    if len(v) != 3:
+        raise ValueError('expected an int or a 3-tuple, got %r' % (v,))
+    return v
+
+
+def spec_struct(module):
+    """hcu_unet_spec for a 3D Unet_Constructor (parameters read from its modules)."""
+    s = module.model_specification
+    if s['image_dimensions'] != 3:
+        raise RuntimeError('unsupported upsampling function', nn.ConvTranspose2d)
+    fs = list(s['feature_sizes'])
+    if len(fs) > _lib.MAX_LEVELS:
+        raise NotImplementedError('at most %d levels are supported' % _lib.MAX_LEVELS)
+    d0 = module.down_steps[0]
+    u0 = module.up_steps[0]
+    spec = _lib.UnetSpec()
+    spec.levels = len(fs)
+    spec.in_channels = d0.conv1.in_channels
+    spec.out_channels = module.out_conv.out_channels
+    for i, f in enumerate(fs):
+        spec.features[i] = f
+    spec.k1 = _lib.c_int3(*d0.conv1.kernel_size)
+    spec.k2 = _lib.c_int3(*d0.conv2.kernel_size)
+    spec.d1 = _lib.c_int3(*d0.conv1.dilation)
+    spec.d2 = _lib.c_int3(*d0.conv2.dilation)
+    spec.g1 = d0.conv1.groups
+    spec.g2 = d0.conv2.groups
+    if len(u0.up_conv.kernel_size) != 3:
+        raise RuntimeError('ConvTranspose3d kernel_size must have 3 elements, got %r'
+                           % (u0.up_conv.kernel_size,))
+    spec.up_k = _lib.c_int3(*u0.up_conv.kernel_size)
+    spec.up_s = _lib.c_int3(*u0.up_conv.stride)
+    spec.pool_k = _lib.c_int3(*_triple(module.max_pool.kernel_size))
+    mp = module.max_pool
+    if _triple(mp.stride) != _triple(mp.kernel_size) or _triple(mp.padding) != (0, 0, 0) \
+            or _triple(mp.dilation) != (1, 1, 1) or mp.ceil_mode:
+        raise NotImplementedError('max_pool must be kernel == stride, no padding, floor mode')
+    bns = bn_modules(module)
+    eps, mom = bns[0].eps, bns[0].momentum
+    for bn in bns:
+        if bn.eps != eps or bn.momentum != mom or not bn.affine or not bn.track_running_stats:
+            raise NotImplementedError('all BatchNorm3d layers must share eps/momentum and be '
+                                      'affine with running statistics')
+    spec.bn_eps = eps
+    spec.bn_momentum = -1.0 if mom is None else mom
+    # every Down/Up must use the same hyper-parameters (true by construction)
+    for blk in list(module.down_steps) + list(module.up_steps):
+        for conv, k, d, g in ((blk.conv1, spec.k1, spec.d1, spec.g1),
+                              (blk.conv2, spec.k2, spec.d2, spec.g2)):
+            if tuple(conv.kernel_size) != tuple(k) or tuple(conv.dilation) != tuple(d) \
+                    or conv.groups != g or tuple(conv.stride) != (1, 1, 1) \
+                    or tuple(conv.padding) != (0, 0, 0):
+                raise NotImplementedError('non-uniform conv hyper-parameters')
+    return spec
+
+
+def bn_modules(module):
+    out = []
+    for blk in module.down_steps:
+        out += [blk.batch1, blk.batch2]
+    for blk in module.up_steps:
+        out += [blk.batch1, blk.batch2]
+    return out
+
+
+class _Plan:
+    def __init__(self, spec, B, X, Y, Z):
+        L = _lib.lib()
+        handle = ctypes.c_void_p()
+        _lib.check(L.hcu_unet_plan_create(ctypes.byref(spec), B, X, Y, Z, ctypes.byref(handle)),
+                   'Unet_Constructor')
+        self.handle = handle
+        out_shape = (ctypes.c_int64 * 5)()
+        n_params = ctypes.c_int64()
+        n_bn = ctypes.c_int()
+        saved = ctypes.c_size_t()
+        scratch = ctypes.c_size_t()
+        _lib.check(L.hcu_unet_plan_query(handle, out_shape, ctypes.byref(n_params),
+                                         ctypes.byref(n_bn), ctypes.byref(saved),
+                                         ctypes.byref(scratch)))
+        self.out_shape = tuple(int(v) for v in out_shape)
+        self.n_params = int(n_params.value)
+        self.n_bn = int(n_bn.value)
+        self.saved_bytes = int(saved.value)
+        self.scratch_bytes = int(scratch.value)
+
+    def __del__(self):
+        try:
+            if self.handle:
+                _lib.lib().hcu_unet_plan_destroy(self.handle)
+        except Exception:
+            pass
+
+
+class _Engine:
+    """Per-module native state: plans per input shape, flat params/grads."""
+
+    def __init__(self, module):
+        self.module_ref = module
+        self.spec = spec_struct(module)
+        self.plans = {}
+        self.flat = None
+        self.grad_flat = None
+        self.params = None
+        self._bn_arrays = None
+
+    def check_input(self, x):
+        m = self.module_ref
+        if x.dim() != 5:
+            raise RuntimeError('Expected 5D input [B, C, X, Y, Z] for conv3d, got %dD' % x.dim())
+        cin = m.down_steps[0].conv1.in_channels
+        if x.shape[1] != cin:
+            raise RuntimeError('Given groups=%d, expected input%s to have %d channels, but got %d '
+                               'channels instead' % (m.down_steps[0].conv1.groups,
+                                                     list(x.shape), cin, x.shape[1]))
+        if x.dtype != torch.float32:
+            raise RuntimeError('Input type (%s) and weight type (float) should be the same' % x.dtype)
+
+    def plan(self, shape):
+        key = tuple(shape)
+        p = self.plans.get(key)
+        if p is None:
+            B, _, X, Y, Z = key
+            p = _Plan(self.spec, B, X, Y, Z)
+            self.plans[key] = p
+        return p
+
+    def params_ready(self):
+        """Ensure every parameter is a view of one flat fp32 device buffer."""
+        m = self.module_ref
+        params = list(m.parameters())
+        flat = self.flat
+        ok = flat is not None and self.params is not None and len(params) == len(self.params)
+        if ok:
+            base = flat.data_ptr()
+            off = 0
+            for p, q in zip(params, self.params):
+                if p is not q or p.data_ptr() != base + 4 * off:
+                    ok = False
+                    break
+                off += p.numel()
+        if not ok:
+            dev = params[0].device
+            for p in params:
+                if p.dtype != torch.float32:
+                    raise RuntimeError('hcunet_amd: parameters must be float32')
+                if p.device != dev:
+                    raise RuntimeError('hcunet_amd: parameters on several devices')
+            _lib.require_device(params[0], 'Unet_Constructor parameters')
+            n = sum(p.numel() for p in params)
+            flat = torch.empty(n, dtype=torch.float32, device=dev)
+            off = 0
+            with torch.no_grad():
+                for p in params:
+                    k = p.numel()
+                    flat[off:off + k].copy_(p.data.reshape(-1))
+                    p.data = flat[off:off + k].view_as(p)
+                    off += k
+            self.flat = flat
+            self.params = params
+            self.grad_flat = None
+            self._bn_arrays = None
+        return self.params
+
+    def bn_arrays(self):
+        if self._bn_arrays is None:
+            bns = bn_modules(self.module_ref)
+            for bn in bns:
+                if bn.running_mean.dtype != torch.float32 or not bn.running_mean.is_contiguous():
+                    raise RuntimeError('hcunet_amd: BatchNorm running stats must be contiguous fp32')
+            n = len(bns)
+            rm = (ctypes.c_void_p * n)(*[bn.running_mean.data_ptr() for bn in bns])
+            rv = (ctypes.c_void_p * n)(*[bn.running_var.data_ptr() for bn in bns])
+            nb = (ctypes.c_void_p * n)(*[bn.num_batches_tracked.data_ptr() for bn in bns])
+            self._bn_arrays = (rm, rv, nb, [bn.running_mean.data_ptr() for bn in bns])
+        else:
+            bns = bn_modules(self.module_ref)
+            if [bn.running_mean.data_ptr() for bn in bns] != self._bn_arrays[3]:
+                self._bn_arrays = None
+                return self.bn_arrays()
+        return self._bn_arrays
+
+    def tensors(self, x, out, saved, scratch, grads=None):
+        rm, rv, nb, _ = self.bn_arrays()
+        t = _lib.UnetTensors()
+        t.x = x.data_ptr()
+        t.out = out.data_ptr() if out is not None else None
+        t.params = self.flat.data_ptr()
+        t.grads = grads.data_ptr() if grads is not None else None
+        t.bn_running_mean = ctypes.cast(rm, ctypes.POINTER(ctypes.c_void_p))
+        t.bn_running_var = ctypes.cast(rv, ctypes.POINTER(ctypes.c_void_p))
+        t.bn_num_batches_tracked = ctypes.cast(nb, ctypes.POINTER(ctypes.c_void_p))
+        t.saved = saved.data_ptr()
+        t.scratch = scratch.data_ptr()
+        return t
+
+    def grad_target(self):
+        """Decide where backward writes parameter gradients.
+
+        Returns (buffer, accumulate, finish) where finish() attaches/adds the
+        gradients with torch's .grad accumulation semantics."""
+        params = self.params
+        if self.grad_flat is None or self.grad_flat.numel() != self.flat.numel() \
+                or self.grad_flat.device != self.flat.device:
+            self.grad_flat = torch.zeros_like(self.flat)
+        G = self.grad_flat
+        base = G.data_ptr()
+        offs = []
+        off = 0
+        for p in params:
+            offs.append(off)
+            off += p.numel()
+        if all(p.grad is None for p in params):
+            def finish():
+                for p, o in zip(params, offs):
+                    if p.requires_grad:
+                        p.grad = G[o:o + p.numel()].view_as(p)
+            return G, 0, finish
+        if all(p.grad is not None and p.grad.data_ptr() == base + 4 * o
+               and p.grad.shape == p.shape for p, o in zip(params, offs)):
+            return G, 1, (lambda: None)
+        tmp = torch.empty_like(self.flat)
+
+        def finish_mixed():
+            for p, o in zip(params, offs):
+                if not p.requires_grad:
+                    continue
+                g = tmp[o:o + p.numel()].view_as(p)
+                if p.grad is None:
+                    p.grad = g.clone()
+                else:
+                    p.grad.add_(g)
+        return tmp, 0, finish_mixed
+
+
+class _UnetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, eng, *params):
+        x = x.contiguous()
+        plan = eng.plan(x.shape)
+        dev = x.device
+        out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
+        saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
+        scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
+        training = 1 if eng.module_ref.training else 0
+        t = eng.tensors(x, out, saved, scratch)
+        _lib.check(_lib.lib().hcu_unet_forward(plan.handle, ctypes.byref(t), training,
+                                               _lib.stream_handle(dev)), 'Unet_Constructor.forward')
+        ctx.eng = eng
+        ctx.plan = plan
+        ctx.training = training
+        ctx.save_for_backward(x, saved)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout):
+        x, saved = ctx.saved_tensors
+        eng, plan = ctx.eng, ctx.plan
+        dev = x.device
+        dout = dout.contiguous()
+        if dout.dtype != torch.float32:
+            dout = dout.float()
+        scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        G, accumulate, finish = eng.grad_target()
+        t = eng.tensors(x, None, saved, scratch, grads=G)
+        _lib.check(_lib.lib().hcu_unet_backward(plan.handle, ctypes.byref(t),
+                                                ctypes.c_void_p(dout.data_ptr()),
+                                                _lib.ptr(dx), ctx.training, accumulate,
+                                                _lib.stream_handle(dev)),
+                   'Unet_Constructor.backward')
+        finish()
+        return (dx, None) + (None,) * len(eng.params)

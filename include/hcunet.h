@@ -1,0 +1,184 @@
+/*
+ * hcunet.h -- C-ABI of the MI355X-native 3D U-Net training hot path.
+ *
+ * This library replaces the arithmetic behind the reference's Python operator
+ * interface for ONE path: hcat.unet.Unet_Constructor forward + backward, the
+ * pixel-weighted BCE loss (hcat.loss.cross_entropy, method='pixel') and the
+ * Adam step that follows it in the reference training pattern.  The reference
+ * binds no native code (it calls stock torch.nn ops), so each entry point below
+ * names the reference symbol whose semantics it implements; the Python host
+ * layer (hcunet_amd/, re-exported as hcat.unet / hcat.loss) binds these through
+ * ctypes.
+ *
+ * Conventions
+ *   - Every pointer is a device (HBM) pointer owned by the caller.  No entry
+ *     point allocates or frees memory; scratch/saved workspaces are sized by the
+ *     *_bytes / *_query functions and passed in.
+ *   - Work is enqueued asynchronously on `stream` (a hipStream_t, 0 = null
+ *     stream).  Launchers are re-entrant across streams: plans are read-only
+ *     after creation.
+ *   - Return value: HCU_OK or an error code; no C++ exception crosses the ABI.
+ *     hcu_last_error() returns a thread-local message for the last failure.
+ *   - Activation tensors handled by the per-op entry points are channels-last
+ *     fp32: [B][X][Y][Z][Cs] with Cs = round_up(C, 4).  The network entry points
+ *     take the reference's NCXYZ ([B][C][X][Y][Z], PyTorch NCDHW) tensors.
+ *   - Weight tensors are always in PyTorch layout: Conv3d [Cout][Cin/g][kx][ky][kz],
+ *     ConvTranspose3d [Cin][Cout][kx][ky][kz].
+ */
+#ifndef HCUNET_H
+#define HCUNET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *hcu_stream_t; /* hipStream_t */
+
+enum {
+  HCU_OK = 0,
+  HCU_ERR_INVALID = 1,     /* bad argument (maps to ValueError / TypeError) */
+  HCU_ERR_SHAPE = 2,       /* shape error   (maps to RuntimeError, as torch raises) */
+  HCU_ERR_HIP = 3,         /* HIP runtime error */
+  HCU_ERR_UNSUPPORTED = 4, /* configuration the reference itself rejects */
+  HCU_ERR_WORKSPACE = 5    /* workspace too small */
+};
+
+enum { HCU_F32 = 0, HCU_F16 = 1, HCU_U8 = 2 };
+
+const char *hcu_last_error(void);
+int hcu_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* Whole-network executor.                                                   */
+/* Replaces: Unet_Constructor.__init__ shape logic  hcat/unet.py:16-123      */
+/*           Unet_Constructor.forward               hcat/unet.py:125-143     */
+/*           Down.forward / Up.forward / crop       hcat/unet.py:263-340     */
+/*           and their autograd backward (torch.nn ops' derivatives).        */
+/* ------------------------------------------------------------------------ */
+#define HCU_MAX_LEVELS 12
+
+typedef struct hcu_unet_spec {
+  int levels;                       /* len(feature_sizes)                   */
+  int in_channels, out_channels;
+  int features[HCU_MAX_LEVELS];     /* feature_sizes                        */
+  int k1[3], k2[3];                 /* kernel['conv1'], kernel['conv2']     */
+  int d1[3], d2[3];                 /* dilation['conv1'], dilation['conv2'] */
+  int g1, g2;                       /* groups['conv1'], groups['conv2']     */
+  int up_k[3], up_s[3];             /* upsample_kernel, upsample_stride     */
+  int pool_k[3];                    /* max_pool_kernel (kernel = stride)    */
+  float bn_eps;                     /* BatchNorm3d eps (1e-5)               */
+  float bn_momentum;                /* 0.1; < 0 means momentum=None         */
+} hcu_unet_spec;
+
+typedef struct hcu_unet_plan hcu_unet_plan;
+
+/* Validates the spec against an input of [B, in_channels, X, Y, Z] and builds
+ * the launch plan.  Fails with HCU_ERR_SHAPE where torch would raise (input
+ * smaller than a kernel, pooled size 0, upsampled tensor larger than the skip
+ * tensor so that torch.cat raises: hcat/unet.py:311-312). */
+int hcu_unet_plan_create(const hcu_unet_spec *spec, int B, int X, int Y, int Z,
+                         hcu_unet_plan **out);
+void hcu_unet_plan_destroy(hcu_unet_plan *plan);
+
+/* out_shape[5] = output [B, out_channels, OX, OY, OZ]; n_params = number of
+ * parameter scalars (flat layout = Unet_Constructor.parameters() order);
+ * n_bn = number of BatchNorm3d modules; saved_bytes = forward->backward
+ * workspace; scratch_bytes = per-call temporary workspace. */
+int hcu_unet_plan_query(const hcu_unet_plan *plan, int64_t *out_shape,
+                        int64_t *n_params, int *n_bn, size_t *saved_bytes,
+                        size_t *scratch_bytes);
+
+typedef struct hcu_unet_tensors {
+  const float *x;          /* [B][Cin][X][Y][Z] fp32                         */
+  float *out;              /* [B][Cout][OX][OY][OZ] fp32                     */
+  const float *params;     /* flat fp32, Unet_Constructor.parameters() order */
+  float *grads;            /* flat fp32, same layout (backward only)         */
+  float *const *bn_running_mean; /* n_bn pointers: down[i].batch1, batch2 ... */
+  float *const *bn_running_var;  /*   then up[j].batch1, batch2 (module order) */
+  int64_t *const *bn_num_batches_tracked;
+  void *saved;             /* saved_bytes   */
+  void *scratch;           /* scratch_bytes */
+} hcu_unet_tensors;
+
+/* training != 0: BatchNorm uses batch statistics and updates running stats
+ * (nn.BatchNorm3d train mode); 0: running statistics (eval mode). */
+int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t,
+                     int training, hcu_stream_t stream);
+
+/* dout: [B][Cout][OX][OY][OZ] gradient of the output.  Writes (accumulate=0)
+ * or adds (accumulate=1) parameter gradients into t->grads; dx (nullable)
+ * receives the input gradient [B][Cin][X][Y][Z].  Must follow a forward with
+ * the same plan, tensors and training flag. */
+int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t,
+                      const float *dout, float *dx, int training,
+                      int accumulate, hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Loss.  Replaces hcat.loss.cross_entropy(pred, mask, pwl, method='pixel')  */
+/* hcat/loss.py:5-101: crop mask/pwl top-left to pred (:51-53), BCE with     */
+/* logits * (pwl + 1) computed in pwl's dtype (:65,71-72), mean (:101).      */
+/* pwl == NULL means weight 2 everywhere (:46-47).                            */
+/* ------------------------------------------------------------------------ */
+size_t hcu_loss_pixel_scratch_bytes(int64_t n_pred);
+/* pred [B][C][PX][PY][PZ] fp32; mask/pwl [B][C][MX][MY][MZ] of dtype
+ * mask_dtype / pwl_dtype (HCU_F32, HCU_F16, HCU_U8).  loss[0] <- mean loss;
+ * dpred <- d(loss)/d(pred) for an upstream gradient of 1 (nullable). */
+int hcu_loss_pixel_fwd(const float *pred, int B, int C, int PX, int PY, int PZ,
+                       const void *mask, int mask_dtype, const void *pwl,
+                       int pwl_dtype, int MX, int MY, int MZ, float *loss,
+                       float *dpred, void *scratch, size_t scratch_bytes,
+                       hcu_stream_t stream);
+/* dst[i] = src[i] * scale[0] (scale is a device scalar: the upstream grad). */
+int hcu_scale_by_device_scalar(const float *src, const float *scale, float *dst,
+                               int64_t n, hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Optimizer.  Replaces torch.optim.Adam.step (tests/r_unet_test.py:24,56)   */
+/* for a flat parameter buffer: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;  */
+/* p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps); L2 weight decay.     */
+/* ------------------------------------------------------------------------ */
+int hcu_adam_step(float *p, const float *g, float *m, float *v, int64_t n,
+                  float lr, float beta1, float beta2, float eps,
+                  float weight_decay, int64_t step, float grad_scale,
+                  hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Per-op entry points (channels-last activations).  Used by the parity     */
+/* tests to localise errors; the network executor calls the same kernels.    */
+/* ------------------------------------------------------------------------ */
+typedef struct hcu_conv_desc {
+  int B, Cin, Cout;        /* logical channels                                */
+  int X, Y, Z;             /* input spatial dims                              */
+  int k[3], stride[3], dil[3];
+  int groups;              /* Conv3d only                                     */
+  int transposed;          /* 0: nn.Conv3d (valid, stride 1 only)
+                              1: nn.ConvTranspose3d (pad 0, dil 1, groups 1) */
+} hcu_conv_desc;
+
+size_t hcu_conv_scratch_bytes(const hcu_conv_desc *d);
+/* Output spatial dims of the op described by d (out[3]). */
+int hcu_conv_out_dims(const hcu_conv_desc *d, int *out);
+/* nn.Conv3d / nn.ConvTranspose3d forward: y = conv(x, w) + bias. */
+int hcu_conv_fwd_cl(const hcu_conv_desc *d, const float *x, const float *w,
+                    const float *bias, float *y, void *scratch,
+                    size_t scratch_bytes, hcu_stream_t stream);
+/* d(input) from d(output). */
+int hcu_conv_dgrad_cl(const hcu_conv_desc *d, const float *dy, const float *w,
+                      float *dx, void *scratch, size_t scratch_bytes,
+                      hcu_stream_t stream);
+/* d(weight), d(bias) (nullable) from input and d(output); overwrite. */
+int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy,
+                      float *dw, float *dbias, void *scratch,
+                      size_t scratch_bytes, hcu_stream_t stream);
+
+/* nn.MaxPool3d(kernel=stride=k, floor mode) forward, channels-last. */
+int hcu_maxpool_fwd_cl(int B, int C, int X, int Y, int Z, const int *k,
+                       const float *x, float *y, hcu_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HCUNET_H */
