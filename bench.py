@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Training throughput of the 5-level 3D U-Net hot path (BASELINE.json metric).
+
+One step = optimizer.zero_grad() -> Unet_Constructor.forward ->
+hcat.loss.cross_entropy(method='pixel') -> backward -> (all-reduce of the flat
+gradient buffer over RCCL when N > 1) -> Adam.step, on synthetic
+[B, 4, 256, 256, 16] volumes resident in HBM (config 2: fp32,
+feature_sizes [8..128], B = 2 per GPU).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints one JSON line (rank 0) with the whole-job voxels/s, the roofline of
+the dominant kernel (HIP-event timing of every launch during a second pass of
+K steps) and the CPU baseline (the oracle restatement of the reference timed
+on this host's cores).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from hcat.loss import cross_entropy  # noqa: E402
+from hcat.unet import Unet_Constructor  # noqa: E402
+import hcunet_amd  # noqa: E402
+from hcunet_amd import _lib  # noqa: E402
+
+METRIC = "training voxels/sec (fwd+bwd+step), 5-level 3D U-Net, 256×256×16×4 tiles"
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, dense
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
+TILE = (256, 256, 16)
+
+CONFIGS = {
+    '2': dict(kw=dict(image_dimensions=3, in_channels=4, out_channels=1,
+                      feature_sizes=[8, 16, 32, 64, 128],
+                      kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)},
+                      upsample_kernel=(2, 2, 2), max_pool_kernel=(2, 2, 1),
+                      upsample_stride=(2, 2, 1)),
+              batch=2, dtype='fp32'),
+}
+
+
+def synth_inputs(B, seed, device):
+    """Synthetic stand-ins for to_float -> normalize -> to_tensor volumes
+    (hcat/transforms.py:105-136): x in [-1, 1), mask Bernoulli(0.5) fp16,
+    pwl U[0, 11) fp16 (w0 = 11, hcat/train/train_utils.py:67)."""
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.randint(0, 65536, (B, 4) + TILE, generator=g).float() / 65536.0 - 0.5) / 0.5
+    mask = (torch.rand((B, 1) + TILE, generator=g) < 0.5).half()
+    pwl = (torch.rand((B, 1) + TILE, generator=g) * 11.0).half()
+    return x.to(device), mask.to(device), pwl.to(device)
+
+
+def cpu_baseline(cfg, x, mask, pwl, budget_s=15.0):
+    """Oracle restatement of the reference step on host cores (bounded sample)."""
+    from oracle import unet_oracle as uo
+    threads = max(1, min(16, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    spec = uo.normalize_spec(**cfg['kw'])
+    state = uo.init_state(spec, 0)
+    x, mask, pwl = x.cpu(), mask.cpu(), pwl.cpu()
+    times = []
+    t_start = time.perf_counter()
+    uo.train_step(spec, state, x, mask, pwl)  # warm-up
+    while len(times) < 3 or (time.perf_counter() - t_start < budget_s and len(times) < 20):
+        t0 = time.perf_counter()
+        r = uo.train_step(spec, state, x, mask, pwl)
+        times.append(time.perf_counter() - t0)
+        state = r['state_after']
+    med = statistics.median(times)
+    vox = x.shape[0] * TILE[0] * TILE[1] * TILE[2]
+    return {"value": vox / med, "unit": "voxels/s", "cores": threads, "kind": "port",
+            "sample": "%d full config-2 train steps (B=%d, fwd+loss+bwd+Adam) of the oracle "
+                      "restatement (torch CPU, %d threads), median %.3f s/step"
+                      % (len(times), x.shape[0], threads, med)}
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/traffic.json, written by tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, 'profiles', 'traffic.json')
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+        return tab.get(kernel, {}).get('hbm_bytes_per_launch')
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='2', choices=sorted(CONFIGS))
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-kernel-timing', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+    cfg = CONFIGS[args.config]
+    B = cfg['batch']
+
+    torch.manual_seed(0)
+    model = Unet_Constructor(**cfg['kw']).to(device).train()
+    hcunet_amd.dist.broadcast_parameters(model)
+    opt = hcunet_amd.optim.Adam(model.parameters(), lr=1e-3)
+    x, mask, pwl = synth_inputs(B, 1000 + rank, device)
+
+    def step():
+        opt.zero_grad()
+        out = model(x)
+        loss = cross_entropy(out, mask, pwl, method='pixel')
+        loss.backward()
+        hcunet_amd.dist.allreduce_gradients(model)
+        opt.step()
+        return loss
+
+    def sync():
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    vox = world * B * TILE[0] * TILE[1] * TILE[2] * args.steps
+    value = vox / elapsed
+
+    roofline = None
+    kernels = None
+    if not args.no_kernel_timing:
+        _lib.lib().hcu_timing_enable(args.steps * 512)
+        for _ in range(args.steps):
+            step()
+        sync()
+        rep = _lib.timing_report()
+        _lib.lib().hcu_timing_disable()
+        total_ms = sum(v['ms'] for v in rep.values())
+        name, d = max(rep.items(), key=lambda kv: kv[1]['ms'])
+        avg_s = d['ms'] / d['count'] / 1e3
+        if d['flops'] > 0:
+            ach = d['flops'] / d['count'] / avg_s / 1e12
+            bound, peak, unit = 'mfma', PEAK_FP32_MFMA_TFLOPS, 'TFLOP/s'
+        else:
+            ach = d['bytes'] / d['count'] / avg_s / 1e9
+            bound, peak, unit = 'hbm', PEAK_HBM_GBS, 'GB/s'
+        roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit,
+                    "frac": ach / peak, "traffic": load_traffic(name), "kernel": name,
+                    "avg_launch_us": avg_s * 1e6,
+                    "launches_per_step": d['count'] / args.steps,
+                    "flops_per_launch": d['flops'] / d['count'],
+                    "share_of_kernel_time": d['ms'] / total_ms}
+        step_flops = sum(v['flops'] for v in rep.values()) / args.steps
+        kernels = {"kernel_ms_per_step": total_ms / args.steps,
+                   "algorithmic_tflops_per_step": step_flops / 1e12,
+                   "step_mfma_tflops": step_flops / (ms_per_step / 1e3) / 1e12,
+                   "top": sorted(({"kernel": k, "ms_per_step": v['ms'] / args.steps,
+                                   "launches_per_step": v['count'] / args.steps}
+                                  for k, v in rep.items()),
+                                 key=lambda r: -r['ms_per_step'])[:8]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, x, mask, pwl)
+
+    if rank == 0:
+        line = {"metric": METRIC, "value": value, "unit": "voxels/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": cfg['dtype'], "data": "synthetic",
+                "config": {"workload": "3D U-Net feature_sizes=[8,16,32,64,128] fp32 train step "
+                                       "(fwd + pixel BCE + bwd + Adam), B=%d per GPU, "
+                                       "%dx%dx%dx4 volumes" % ((B,) + TILE),
+                           "global_batch": B * world, "per_gpu_batch": B,
+                           "parallelism": "dp%d" % world, "final_loss": final_loss},
+                "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -86,6 +86,9 @@ SYMBOLS = [
     ("hcu_conv_dgrad_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("hcu_conv_wgrad_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("hcu_maxpool_fwd_cl", _I, [_I, _I, _I, _I, _I, ctypes.POINTER(_I), _VP, _VP, _VP]),
+    ("hcu_timing_enable", _I, [_I]),
+    ("hcu_timing_disable", _I, []),
+    ("hcu_timing_report", _I64, [ctypes.c_char_p, _I64]),
 ]
 
 _lib = None
@@ -143,3 +146,17 @@ def require_device(t, what):
         raise RuntimeError(
             "hcunet_amd: %s is on %s; the MI355X path runs on ROCm devices only "
             "(move the module and tensors with .to('cuda'))" % (what, t.device))
+
+
+def timing_report():
+    """Per-kernel-symbol totals recorded since hcu_timing_enable():
+    {name: dict(count, ms, flops, bytes)} (synchronises the recorded events)."""
+    L = lib()
+    n = L.hcu_timing_report(None, 0)
+    buf = ctypes.create_string_buffer(int(n) + 1)
+    L.hcu_timing_report(buf, n + 1)
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, cnt, ms, fl, by = line.split('\t')
+        out[name] = dict(count=int(cnt), ms=float(ms), flops=float(fl), bytes=float(by))
+    return out

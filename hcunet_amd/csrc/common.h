@@ -54,6 +54,7 @@ struct GConvArgs {
   int HX, HY, HZ, P;
   int CK, NSUB, MPW;
   int lds_bytes;
+  double flops;                       // algorithmic FLOPs (0: derive)
 };
 // Chooses the tile and kernel variant; returns 0 or an error code.
 int plan_gconv(GConvArgs &a, int target_blocks);
@@ -84,8 +85,11 @@ struct WGradArgs {
   int TX, TY, TZ, ntx, nty, ntz;
   int HAX, HAY, HAZ, PA, HGX, HGY, HGZ, PG;
   int CKA, CKG, mloc, nloc, MS, NS;
+  int TA, TG;                         // taps per block (rows / cols mode)
+  int nci, nco, ntc;                  // channel chunks and tap chunks
   int mchunks, nchunks, KB;
   int lds_bytes;
+  double flops;                       // algorithmic FLOPs (0: derive)
 };
 int plan_wgrad(WGradArgs &a, int target_blocks);
 int launch_wgrad(const WGradArgs &a, hipStream_t s);

@@ -14,6 +14,7 @@
 // Replaces the arithmetic of nn.Conv3d / nn.ConvTranspose3d forward and their
 // input gradients on the reference path (hcat/unet.py:246-257, 281-298).
 #include "common.h"
+#include "timing.h"
 #include <algorithm>
 #include <cmath>
 
@@ -281,14 +282,27 @@ int plan_gconv(GConvArgs &a, int target_blocks) {
   return 0;
 }
 
-#define GCONV_CASE(CK_, NS_, MP_)                                                          \
-  if (a.CK == CK_ && a.NSUB == NS_ && a.MPW == MP_) {                                      \
-    hipLaunchKernelGGL((gconv_kernel<CK_, NS_, MP_>), grid, dim3(256), a.lds_bytes, s, a); \
-    HCU_CHECK_LAUNCH();                                                                    \
-    return 0;                                                                              \
+#define GCONV_CASE(CK_, NS_, MP_)                                                            \
+  if (a.CK == CK_ && a.NSUB == NS_ && a.MPW == MP_) {                                        \
+    HCU_TIMED(s, "gconv_kernel<" #CK_ "," #NS_ "," #MP_ ">", gconv_flops(a), gconv_bytes(a),  \
+              hipLaunchKernelGGL((gconv_kernel<CK_, NS_, MP_>), grid, dim3(256), a.lds_bytes, \
+                                 s, a));                                                     \
+    HCU_CHECK_LAUNCH();                                                                      \
+    return 0;                                                                                \
   }
 #define GCONV_MP(CK_, NS_) GCONV_CASE(CK_, NS_, 1) GCONV_CASE(CK_, NS_, 2) GCONV_CASE(CK_, NS_, 4)
 #define GCONV_NS(CK_) GCONV_MP(CK_, 1) GCONV_MP(CK_, 2) GCONV_MP(CK_, 4)
+
+// Algorithmic work of one launch: useful MACs (x2) and compulsory HBM bytes
+// (input + output tensors read/written once, weights once).
+static double gconv_flops(const GConvArgs &a) {
+  if (a.flops > 0) return a.flops;
+  return 2.0 * a.B * a.OX * a.OY * a.OZ * (double)a.Cout * a.KX * a.KY * a.KZ * a.ICs;
+}
+static double gconv_bytes(const GConvArgs &a) {
+  return 4.0 * ((double)a.B * a.IX * a.IY * a.IZ * a.ICs + (double)a.B * a.OX * a.OY * a.OZ * a.OCs +
+                (double)a.KX * a.KY * a.KZ * a.ICs * a.Cout);
+}
 
 int launch_gconv(const GConvArgs &a, hipStream_t s) {
   const dim3 grid(a.ntx * a.nty * a.ntz, a.CoutW / (a.NSUB * 16), a.B);

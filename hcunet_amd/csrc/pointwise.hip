@@ -9,6 +9,7 @@
 // kernel sums in fp64 in a fixed order: results are bitwise reproducible run to
 // run (no float atomics anywhere).
 #include "common.h"
+#include "timing.h"
 #include <algorithm>
 
 namespace hcu {
@@ -89,9 +90,9 @@ int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
                            float *run_mean, float *run_var, int64_t *nbt,
                            float eps, float momentum, int training, BNCoef coef,
                            hipStream_t s) {
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, stats, R,
+  HCU_TIMED(s, "bn_fwd_finalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, stats, R,
                      statsW, C, count, gamma, beta, run_mean, run_var, nbt, eps,
-                     momentum, training, coef);
+                     momentum, training, coef));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -143,8 +144,8 @@ bn_bwd_finalize_kernel(const float *part, int R, int C, int Cs, double count,
 int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, double count,
                            BNCoef coef, float *dgamma, float *dbeta, int training,
                            int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, part, R, C,
-                     Cs, count, coef, dgamma, dbeta, training, accumulate);
+  HCU_TIMED(s, "bn_bwd_finalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, part, R, C,
+                     Cs, count, coef, dgamma, dbeta, training, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -206,8 +207,8 @@ int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
                        int kz, hipStream_t s) {
   const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
   const int64_t n = (int64_t)B * PX * PY * PZ * (Cs / 4);
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, scale,
-                     shift, p, B, X, Y, Z, Cs, kx, ky, kz, PX, PY, PZ);
+  HCU_TIMED(s, "maxpool_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, scale,
+                     shift, p, B, X, Y, Z, Cs, kx, ky, kz, PX, PY, PZ));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -295,8 +296,8 @@ bn_bwd_reduce_dense_kernel(float *dA, const float *y, BNCoef coef, int64_t nvox,
 int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef, int64_t nvox,
                                int Cs, float *part, int R, hipStream_t s) {
   const RedGeom g = red_geom(nvox, Cs, R);
-  hipLaunchKernelGGL(bn_bwd_reduce_dense_kernel, dim3(R), dim3(256),
-                     (size_t)std::max(g.tb, 256) * 8 * 4, s, dA, y, coef, nvox, Cs, part, g);
+  HCU_TIMED(s, "bn_bwd_reduce_dense_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_reduce_dense_kernel, dim3(R), dim3(256),
+                     (size_t)std::max(g.tb, 256) * 8 * 4, s, dA, y, coef, nvox, Cs, part, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -372,9 +373,9 @@ int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, floa
                               int B, int X, int Y, int Z, int Cs, int kx, int ky,
                               int kz, float *part, int R, hipStream_t s) {
   const RedGeom g = red_geom((int64_t)B * X * Y * Z, Cs, R);
-  hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
+  HCU_TIMED(s, "bn_bwd_reduce_pool_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
                      (size_t)std::max(g.tb, 256) * 8 * 4, s, dP, y, coef, dz, B, X, Y, Z,
-                     Cs, kx, ky, kz, part, g);
+                     Cs, kx, ky, kz, part, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -399,8 +400,8 @@ bn_bwd_apply_kernel(float *dz, const float *y, BNCoef coef, int64_t n4, int C4) 
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, int Cs,
                         hipStream_t s) {
   const int64_t n4 = nvox * (Cs / 4);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, s, dz, y,
-                     coef, n4, Cs / 4);
+  HCU_TIMED(s, "bn_bwd_apply_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, s, dz, y,
+                     coef, n4, Cs / 4));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -439,8 +440,8 @@ int launch_outconv_fwd(const float *y, BNCoef coef, const float *w, const float 
                        float *pred, int B, int64_t V, int C, int Cs, int Co,
                        hipStream_t s) {
   if (Co > MAXCO) return fail(4, "out_conv: out_channels > 4 not supported");
-  hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for((int64_t)B * V)), dim3(256), 0, s,
-                     y, coef, w, bias, pred, B, V, C, Cs, Co);
+  HCU_TIMED(s, "outconv_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for((int64_t)B * V)), dim3(256), 0, s,
+                     y, coef, w, bias, pred, B, V, C, Cs, Co));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -522,8 +523,8 @@ int launch_outconv_bwd(const float *dpred, const float *y, BNCoef coef, const fl
   if (Co > MAXCO) return fail(4, "out_conv: out_channels > 4 not supported");
   const RedGeom g = red_geom((int64_t)B * V, Cs, R);
   const size_t lds = (size_t)std::max(g.tb, 256) * (8 + 5 * MAXCO) * 4;
-  hipLaunchKernelGGL(outconv_bwd_kernel, dim3(R), dim3(256), lds, s, dpred, y, coef, w,
-                     dz, B, V, C, Cs, Co, part_bn, part_oc, g);
+  HCU_TIMED(s, "outconv_bwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_bwd_kernel, dim3(R), dim3(256), lds, s, dpred, y, coef, w,
+                     dz, B, V, C, Cs, Co, part_bn, part_oc, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -550,8 +551,8 @@ chansum_kernel(const float *x, int Cs, float *part, RedGeom g) {
 
 int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R, hipStream_t s) {
   const RedGeom g = red_geom(nvox, Cs, R);
-  hipLaunchKernelGGL(chansum_kernel, dim3(R), dim3(256), (size_t)std::max(g.tb, 256) * 4 * 4,
-                     s, x, Cs, part, g);
+  HCU_TIMED(s, "chansum_kernel", 0.0, 0.0, hipLaunchKernelGGL(chansum_kernel, dim3(R), dim3(256), (size_t)std::max(g.tb, 256) * 4 * 4,
+                     s, x, Cs, part, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -567,8 +568,8 @@ reduce_partials_kernel(const float *part, int R, int W, int n, float *out, int a
 
 int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
                            int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, R,
-                     W, n, out, accumulate);
+  HCU_TIMED(s, "reduce_partials_kernel", 0.0, 0.0, hipLaunchKernelGGL(reduce_partials_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, R,
+                     W, n, out, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -595,7 +596,7 @@ to_cl_kernel(const float *x, float *xcl, int B, int C, int Cs, int64_t V) {
 
 int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s) {
   const int64_t n = (int64_t)B * (Cs / 4) * V;
-  hipLaunchKernelGGL(to_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xcl, B, C, Cs, V);
+  HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0, hipLaunchKernelGGL(to_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xcl, B, C, Cs, V));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -615,7 +616,7 @@ from_cl_kernel(const float *xcl, float *x, int B, int C, int Cs, int64_t V) {
 
 int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V, hipStream_t s) {
   const int64_t n = (int64_t)B * C * V;
-  hipLaunchKernelGGL(from_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, xcl, x, B, C, Cs, V);
+  HCU_TIMED(s, "from_cl_kernel", 0.0, 0.0, hipLaunchKernelGGL(from_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, xcl, x, B, C, Cs, V));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -652,8 +653,8 @@ int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int gro
                          int fold_mod, int T, int ECs, int CoutW, hipStream_t s) {
   const int E = std::min(fold_mod, groups * Cin_g);
   const int64_t n = (int64_t)T * ECs * CoutW;
-  hipLaunchKernelGGL(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
-                     Cin_g, groups, fold_mod, T, ECs, CoutW, E);
+  HCU_TIMED(s, "prep_conv_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
+                     Cin_g, groups, fold_mod, T, ECs, CoutW, E));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -677,8 +678,8 @@ prep_conv_dgrad_kernel(const float *w, float *wg, int Cout, int Cin_g, int group
 int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g, int groups,
                            int fold_mod, int T, int OCs, int EW, int E, hipStream_t s) {
   const int64_t n = (int64_t)T * OCs * EW;
-  hipLaunchKernelGGL(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
-                     Cin_g, groups, fold_mod, T, OCs, EW, E);
+  HCU_TIMED(s, "prep_conv_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
+                     Cin_g, groups, fold_mod, T, OCs, EW, E));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -709,8 +710,8 @@ int launch_prep_convt_fwd(const float *w, float *wg, int Cin, int Cout, int KX, 
                           int KZ, int sx, int sy, int sz, int px, int py, int pz, int Jx,
                           int Jy, int Jz, int ICs, int CoutW, hipStream_t s) {
   const int64_t n = (int64_t)Jx * Jy * Jz * ICs * CoutW;
-  hipLaunchKernelGGL(prep_convt_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
-                     Cout, KX, KY, KZ, sx, sy, sz, px, py, pz, Jx, Jy, Jz, ICs, CoutW);
+  HCU_TIMED(s, "prep_convt_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_convt_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
+                     Cout, KX, KY, KZ, sx, sy, sz, px, py, pz, Jx, Jy, Jz, ICs, CoutW));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -732,8 +733,8 @@ prep_convt_dgrad_kernel(const float *w, float *wg, int Cin, int Cout, int T, int
 int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
                             int CinW, hipStream_t s) {
   const int64_t n = (int64_t)T * UCs * CinW;
-  hipLaunchKernelGGL(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
-                     Cout, T, UCs, CinW);
+  HCU_TIMED(s, "prep_convt_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
+                     Cout, T, UCs, CinW));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -763,8 +764,8 @@ outconv_wfinalize_kernel(const float *part, int R, int Co, int C, int Cs, float 
 int launch_outconv_wfinalize(const float *part_oc, int R, int Co, int C, int Cs, float *dw,
                              float *db, int accumulate, hipStream_t s) {
   const int n = Co * C + Co;
-  hipLaunchKernelGGL(outconv_wfinalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part_oc,
-                     R, Co, C, Cs, dw, db, accumulate);
+  HCU_TIMED(s, "outconv_wfinalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_wfinalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part_oc,
+                     R, Co, C, Cs, dw, db, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -784,7 +785,7 @@ int launch_bn_count_increment(int64_t *const *ptrs, int n, hipStream_t s) {
   CountPtrs c{};
   for (int i = 0; i < n; ++i) c.p[i] = ptrs[i];
   c.n = n;
-  hipLaunchKernelGGL(bn_count_kernel, dim3(1), dim3(64), 0, s, c);
+  HCU_TIMED(s, "bn_count_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_count_kernel, dim3(1), dim3(64), 0, s, c));
   HCU_CHECK_LAUNCH();
   return 0;
 }

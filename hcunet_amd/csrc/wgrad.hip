@@ -11,6 +11,7 @@
 // the PyTorch weight layout, undoing the cat(U,U) weight fold
 // (hcat/unet.py:310-313) and the grouped-conv block diagonal.
 #include "common.h"
+#include "timing.h"
 #include <algorithm>
 
 namespace hcu {
@@ -19,10 +20,23 @@ template <int NS, int MSMAX>
 __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kb = blockIdx.x, mc = blockIdx.y, nc = blockIdx.z;
+  const int kb = blockIdx.x;
   const int T = a.KX * a.KY * a.KZ;
   const int CKA = a.CKA, CKG = a.CKG;
-  const int ci0 = mc * CKA, co0 = nc * CKG;
+  // block -> (tap chunk, channel chunks)
+  int tapc, cic, coc;
+  if (a.taps_rows) {
+    tapc = blockIdx.y / a.nci;
+    cic = blockIdx.y % a.nci;
+    coc = blockIdx.z;
+  } else {
+    cic = blockIdx.y;
+    tapc = blockIdx.z / a.nco;
+    coc = blockIdx.z % a.nco;
+  }
+  const int ci0 = cic * CKA, co0 = coc * CKG;
+  const int t0 = tapc * (a.taps_rows ? a.TA : a.TG);
+  const bool bias_block = a.bias_row && tapc == 0 && cic == 0;
   const int PA = a.PA, PG = a.PG;
   float *alds = smem;
   float *glds = smem + CKA * PA;
@@ -36,13 +50,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
     const int lr = ms * 16 + (lane & 15);
     int off = -2;
     if (a.taps_rows) {
-      const int ta = lr / CKA, c = lr % CKA;
-      if (ta < T) {
-        if (ci0 + c < a.ACs) {
+      const int tl = lr / CKA, c = lr % CKA, ta = t0 + tl;
+      if (tl < a.TA) {
+        if (ta < T && ci0 + c < a.ACs) {
           const int kz = ta % a.KZ, q = ta / a.KZ, ky = q % a.KY, kx = q / a.KY;
           off = c * PA + kx * a.adx * HAYZ + ky * a.ady * HAZ + kz * a.adz;
         }
-      } else if (a.bias_row && mc == 0 && lr == T * CKA) {
+      } else if (bias_block && lr == a.TA * CKA) {
         off = -1;
       }
     } else {
@@ -58,8 +72,8 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
     if (a.taps_rows) {
       if (lc < CKG && co0 + lc < a.GCs) off = lc * PG;
     } else {
-      const int tg = lc / CKG, o = lc % CKG;
-      if (tg < T && co0 + o < a.GCs) {
+      const int tl = lc / CKG, o = lc % CKG, tg = t0 + tl;
+      if (tl < a.TG && tg < T && co0 + o < a.GCs) {
         const int kz = tg % a.KZ, q = tg / a.KZ, ky = q % a.KY, kx = q / a.KY;
         off = o * PG + kx * a.gdx * HGYZ + ky * a.gdy * HGZ + kz * a.gdz;
       }
@@ -187,17 +201,18 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
     const int lc = ns * 16 + (ln & 15);
     int grow = -1, gcol = -1;
     if (a.taps_rows) {
-      if (lr < T * CKA) {
+      const int tl = lr / CKA, ta = t0 + tl;
+      if (tl < a.TA) {
         const int ci = ci0 + lr % CKA;
-        if (ci < a.ACs) grow = (lr / CKA) * a.ACs + ci;
-      } else if (a.bias_row && mc == 0 && lr == T * CKA) {
+        if (ta < T && ci < a.ACs) grow = ta * a.ACs + ci;
+      } else if (bias_block && lr == a.TA * CKA) {
         grow = T * a.ACs;
       }
       if (lc < CKG && co0 + lc < a.GCs) gcol = co0 + lc;
     } else {
       if (lr < CKA && ci0 + lr < a.ACs) grow = ci0 + lr;
-      const int tg = lc / CKG, o = lc % CKG;
-      if (tg < T && co0 + o < a.GCs) gcol = tg * a.GCs + co0 + o;
+      const int tl = lc / CKG, o = lc % CKG, tg = t0 + tl;
+      if (tl < a.TG && tg < T && co0 + o < a.GCs) gcol = tg * a.GCs + co0 + o;
     }
     if (grow >= 0 && gcol >= 0)
       a.partial[((size_t)kb * a.Mtot + grow) * a.Ntot + gcol] = red[idx];
@@ -212,31 +227,48 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   a.NS = 0;
   for (int i = 0; i < 3; ++i) {
     const int NS = nss[i], MSMAX = 16 / NS;
+    const int rows = MSMAX * 16, cols = NS * 16;
     if (a.taps_rows) {
       if (NS > 1 && (NS / 2) * 16 >= a.GCs) continue;  // do not waste columns
-      int cka = ((MSMAX * 16 - (a.bias_row ? 1 : 0)) / T) / 4 * 4;
+      const int brow = a.bias_row ? 1 : 0;
+      int cka = ((rows - brow) / T) / 4 * 4;
+      int ta = T;
+      if (cka < 4) {  // too many taps for one block: split the taps
+        cka = 4;
+        ta = (rows - brow) / 4;
+      }
       cka = std::min(cka, a.ACs);
-      if (cka < 4) continue;
       a.CKA = cka;
-      a.CKG = std::min(a.GCs, NS * 16);
-      a.mloc = T * cka + (a.bias_row ? 1 : 0);
+      a.TA = ta;
+      a.TG = 1;
+      a.CKG = std::min(a.GCs, cols);
+      a.mloc = ta * cka + brow;
       a.nloc = a.CKG;
     } else {
-      int ckg = (NS * 16 / T) / 4 * 4;
+      int ckg = (cols / T) / 4 * 4;
+      int tg = T;
+      if (ckg < 4) {
+        ckg = 4;
+        tg = cols / 4;
+      }
       ckg = std::min(ckg, a.GCs);
-      if (ckg < 4) continue;
       a.CKG = ckg;
-      a.CKA = std::min(a.ACs, MSMAX * 16);
+      a.TG = tg;
+      a.TA = 1;
+      a.CKA = std::min(a.ACs, rows);
       a.mloc = a.CKA;
-      a.nloc = T * ckg;
+      a.nloc = tg * ckg;
     }
     a.NS = NS;
     a.MS = cdiv(a.mloc, 16);
     break;
   }
-  if (!a.NS) return fail(4, "wgrad: kernel too large for the tile");
-  a.mchunks = cdiv(a.ACs, a.CKA);
-  a.nchunks = cdiv(a.GCs, a.CKG);
+  if (!a.NS) return fail(4, "wgrad: no tile");
+  a.nci = cdiv(a.ACs, a.CKA);
+  a.nco = cdiv(a.GCs, a.CKG);
+  a.ntc = a.taps_rows ? cdiv(T, a.TA) : cdiv(T, a.TG);
+  a.mchunks = a.taps_rows ? a.ntc * a.nci : a.nci;
+  a.nchunks = a.taps_rows ? a.nco : a.ntc * a.nco;
   a.Mtot = a.taps_rows ? T * a.ACs + (a.bias_row ? 1 : 0) : a.ACs;
   a.Ntot = a.taps_rows ? a.GCs : T * a.GCs;
   const int ntz = cdiv(a.PZ, 16);
@@ -282,12 +314,21 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
 
 int launch_wgrad(const WGradArgs &a, hipStream_t s) {
   const dim3 grid(a.KB, a.mchunks, a.nchunks);
+  const int T = a.KX * a.KY * a.KZ;
+  const double fl = a.flops > 0 ? a.flops
+                                : 2.0 * a.B * a.PX * a.PY * a.PZ * (double)T * a.ACs * a.GCs;
+  const double by = 4.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
+                           (double)a.B * a.GX * a.GY * a.GZ * a.GCs +
+                           (double)wgrad_partial_floats(a));
   if (a.NS == 4) {
-    hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, dim3(256), a.lds_bytes, s, a);
+    HCU_TIMED(s, "wgrad_kernel<4,4>", fl, by,
+              hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, dim3(256), a.lds_bytes, s, a));
   } else if (a.NS == 2) {
-    hipLaunchKernelGGL((wgrad_kernel<2, 8>), grid, dim3(256), a.lds_bytes, s, a);
+    HCU_TIMED(s, "wgrad_kernel<2,8>", fl, by,
+              hipLaunchKernelGGL((wgrad_kernel<2, 8>), grid, dim3(256), a.lds_bytes, s, a));
   } else {
-    hipLaunchKernelGGL((wgrad_kernel<1, 16>), grid, dim3(256), a.lds_bytes, s, a);
+    HCU_TIMED(s, "wgrad_kernel<1,16>", fl, by,
+              hipLaunchKernelGGL((wgrad_kernel<1, 16>), grid, dim3(256), a.lds_bytes, s, a));
   }
   HCU_CHECK_LAUNCH();
   return 0;
@@ -331,7 +372,8 @@ __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize
 int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f);
+  HCU_TIMED(s, "wgrad_finalize_kernel", 0.0, 4.0 * (double)n * (f.KB + 1),
+            hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f));
   HCU_CHECK_LAUNCH();
   return 0;
 }

@@ -178,6 +178,15 @@ int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy,
 int hcu_maxpool_fwd_cl(int B, int C, int X, int Y, int Z, const int *k,
                        const float *x, float *y, hcu_stream_t stream);
 
+/* ------------------------------------------------------------------------ */
+/* Measurement: opt-in HIP-event timing of every library launch (bench.py). */
+/* ------------------------------------------------------------------------ */
+int hcu_timing_enable(int max_launches);
+int hcu_timing_disable(void);
+/* One line per kernel symbol: name\tcount\ttotal_ms\tflops\tbytes (totals
+ * over launches; flops/bytes are algorithmic).  Returns bytes needed. */
+int64_t hcu_timing_report(char *buf, int64_t len);
+
 #ifdef __cplusplus
 }
 #endif
