@@ -88,6 +88,7 @@ SYMBOLS = [
     ("hcu_maxpool_fwd_cl", _I, [_I, _I, _I, _I, _I, ctypes.POINTER(_I), _VP, _VP, _VP]),
     ("hcu_timing_enable", _I, [_I]),
     ("hcu_timing_disable", _I, []),
+    ("hcu_timing_detail", _I, [_I]),
     ("hcu_timing_report", _I64, [ctypes.c_char_p, _I64]),
 ]
 

@@ -14,6 +14,27 @@ inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 
+// Division by a runtime-constant divisor without the ~40-instruction integer
+// divide: q = (umulhi(n, m) + n) >> s, exact for 0 <= n < 2^31, d >= 1.
+struct FastDiv {
+  uint32_t d = 1, m = 0, s = 0;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t div) : d(div) {
+    s = 0;
+    while ((1ull << s) < div) ++s;
+    m = (uint32_t)((((1ull << s) - div) << 32) / div + 1);
+  }
+  __host__ __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)((((uint64_t)n * m >> 32) + n) >> s);  // v_mul_hi_u32 on device
+  }
+  // q = n / d, r = n % d
+  __host__ __device__ __forceinline__ void divmod(uint32_t n, int &q, int &r) const {
+    const uint32_t qq = div(n);
+    q = (int)qq;
+    r = (int)(n - qq * d);
+  }
+};
+
 // Thread-local error message (hcu_last_error()).
 void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
@@ -54,6 +75,7 @@ struct GConvArgs {
   int HX, HY, HZ, P;
   int CK, NSUB, MPW;
   int lds_bytes;
+  FastDiv fHZ, fHY, fTZ, fTY;         // halo / tile index decomposition
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 // Chooses the tile and kernel variant; returns 0 or an error code.
@@ -89,6 +111,7 @@ struct WGradArgs {
   int nci, nco, ntc;                  // channel chunks and tap chunks
   int mchunks, nchunks, KB;
   int lds_bytes;
+  FastDiv fHAZ, fHAY, fHGZ, fHGY, fTZ, fTY;
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 int plan_wgrad(WGradArgs &a, int target_blocks);

@@ -51,10 +51,9 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
     const int i = (wave + 4 * j) * 16 + (lane & 15);
     int v = 0;
     if (i < MT) {
-      const int lz = i % a.TZ;
-      const int r = i / a.TZ;
-      const int ly = r % a.TY;
-      const int lx = r / a.TY;
+      int r, lz, lx, ly;
+      a.fTZ.divmod(i, r, lz);
+      a.fTY.divmod(r, lx, ly);
       v = lx * a.sx * HYZ + ly * a.sy * HZ + lz * a.sz;
     }
     vb[j] = v;
@@ -76,10 +75,9 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
     for (int idx = tid; idx < HV * C4; idx += 256) {
       const int c4 = idx % C4;
       const int v = idx / C4;
-      const int hz = v % HZ;
-      const int t2 = v / HZ;
-      const int hy = t2 % a.HY;
-      const int hx = t2 / a.HY;
+      int t2, hz, hx, hy;
+      a.fHZ.divmod(v, t2, hz);
+      a.fHY.divmod(t2, hx, hy);
       const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
       float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
       if ((unsigned)gx < (unsigned)a.IX && (unsigned)gy < (unsigned)a.IY &&
@@ -116,11 +114,10 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
     __syncthreads();
 
     // ---- MFMA over taps x channels of this chunk
-    for (int t = 0; t < T; ++t) {
-      const int kz = t % a.KZ;
-      const int t2 = t / a.KZ;
-      const int ky = t2 % a.KY;
-      const int kx = t2 / a.KY;
+    int t = 0;
+    for (int kx = 0; kx < a.KX; ++kx)
+    for (int ky = 0; ky < a.KY; ++ky)
+    for (int kz = 0; kz < a.KZ; ++kz, ++t) {
       const int toff = kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz;
 #pragma unroll
       for (int k4 = 0; k4 < C4; ++k4) {
@@ -161,10 +158,9 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int i = m * 16 + (lane >> 4) * 4 + r;
         if (i < MT) {
-          const int lz = i % a.TZ;
-          const int q = i / a.TZ;
-          const int ly = q % a.TY;
-          const int lx = q / a.TY;
+          int q, lz, lx, ly;
+          a.fTZ.divmod(i, q, lz);
+          a.fTY.divmod(q, lx, ly);
           const int ox = ox0 + lx, oy = oy0 + ly, oz = oz0 + lz;
           if (ox < a.OX && oy < a.OY && oz < a.OZ) {
             const size_t ob =
@@ -278,6 +274,10 @@ int plan_gconv(GConvArgs &a, int target_blocks) {
     }
   }
   if (!a.CK) return fail(4, "gconv: no tile fits in LDS");
+  a.fHZ = FastDiv(a.HZ);
+  a.fHY = FastDiv(a.HY);
+  a.fTZ = FastDiv(a.TZ);
+  a.fTY = FastDiv(a.TY);
   if (a.lds_bytes < 4 * NT * 2 * 4) a.lds_bytes = 4 * NT * 2 * 4;
   return 0;
 }

@@ -21,6 +21,8 @@ struct Rec {
 };
 std::mutex g_mu;
 bool g_on = false;
+bool g_detail = false;
+thread_local std::string g_tag;
 std::vector<hipEvent_t> g_pool;
 std::vector<Rec> g_recs;
 size_t g_next = 0;
@@ -28,13 +30,17 @@ size_t g_next = 0;
 
 bool timing_on() { return g_on; }
 
+void timing_set_tag(const char *tag) {
+  if (g_on) g_tag = tag ? tag : "";
+}
+
 int timing_begin(hipStream_t s, const std::string &name, double flops, double bytes) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_on || g_next + 2 > g_pool.size()) return -1;
   const int ev = (int)g_next;
   g_next += 2;
   (void)hipEventRecord(g_pool[ev], s);
-  g_recs.push_back(Rec{name, flops, bytes, ev});
+  g_recs.push_back(Rec{g_detail && !g_tag.empty() ? name + "@" + g_tag : name, flops, bytes, ev});
   return ev;
 }
 
@@ -58,6 +64,12 @@ int hcu_timing_enable(int max_launches) {
   g_pool.resize((size_t)max_launches * 2);
   for (auto &e : g_pool) HCU_HIP(hipEventCreate(&e));
   g_on = true;
+  return HCU_OK;
+}
+
+int hcu_timing_detail(int on) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_detail = on != 0;
   return HCU_OK;
 }
 

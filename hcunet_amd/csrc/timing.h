@@ -3,6 +3,8 @@
 #include <string>
 namespace hcu {
 bool timing_on();
+// Layer tag appended to the kernel name ("kernel@tag") when detail is on.
+void timing_set_tag(const char *tag);
 int timing_begin(hipStream_t s, const std::string &name, double flops, double bytes);
 void timing_end(hipStream_t s, int ev);
 // Bracket one launch statement with timing events when timing is enabled.

@@ -18,6 +18,7 @@
 // conv(U, W[:, :C] + W[:, C:]) (per group), halving that layer's work; the
 // weight gradient is scattered back to both halves.
 #include "common.h"
+#include "timing.h"
 #include "../../include/hcunet.h"
 #include <algorithm>
 #include <cstring>
@@ -77,6 +78,7 @@ struct BNLayer {
 };
 
 struct ConvLayer {
+  std::string name;  // layer tag for per-layer timing ("d0.c1", "u3.c2", ...)
   int Cout = 0, Cin_g = 0, groups = 1, fold_mod = 0, E = 0, T = 0;
   int K[3], D[3];
   int64_t w_off = 0, b_off = 0;
@@ -88,6 +90,7 @@ struct ConvLayer {
 };
 
 struct ConvTLayer {
+  std::string name;
   int Cin = 0, Cout = 0, T = 0;
   int K[3], S[3];
   int64_t w_off = 0, b_off = 0;
@@ -341,6 +344,8 @@ int build_plan(hcu_unet_plan &p) {
     if (cin % s.g1 || f % s.g1 || f % s.g2)
       return fail(HCU_ERR_INVALID, "in_channels/out_channels must be divisible by groups");
     ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
+    c1.name = "d" + std::to_string(i) + ".c1";
+    c2.name = "d" + std::to_string(i) + ".c2";
     c1.w_off = off; off += (int64_t)f * (cin / s.g1) * T1;
     c1.b_off = off; off += f;
     c2.w_off = off; off += (int64_t)f * (f / s.g2) * T2;
@@ -358,6 +363,9 @@ int build_plan(hcu_unet_plan &p) {
       return fail(HCU_ERR_INVALID, "in_channels/out_channels must be divisible by groups");
     ConvLayer &c1 = p.uc1[j], &c2 = p.uc2[j];
     ConvTLayer &u = p.up[j];
+    c1.name = "u" + std::to_string(j) + ".c1";
+    c2.name = "u" + std::to_string(j) + ".c2";
+    u.name = "u" + std::to_string(j) + ".up";
     c1.w_off = off; off += (int64_t)o * (f / s.g1) * T1;
     c1.b_off = off; off += o;
     c2.w_off = off; off += (int64_t)o * (o / s.g2) * T2;
@@ -454,9 +462,14 @@ struct Ctx {
   float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
 };
 
+void tag(const std::string &layer, const char *phase) {
+  if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
+}
+
 int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float *isc,
                  const float *ish, int training) {
   HCU_HIP(hipGetLastError());
+  tag(L.name, "fwd");
   if (int e = launch_prep_conv_fwd(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups, L.fold_mod,
                                    L.T, L.fwd.ICs, L.fwd.CoutW, c.s))
     return e;
@@ -480,6 +493,7 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
 int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, float *dA, int accumulate) {
+  tag(L.name, "wgrad");
   WGradArgs w = L.wg;
   w.A = A;
   w.a_scale = asc;
@@ -504,6 +518,7 @@ int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float 
   f.accumulate = accumulate;
   if (int e = launch_wgrad_finalize(f, c.s)) return e;
   if (!dA) return 0;
+  tag(L.name, "dgrad");
   if (int e = launch_prep_conv_dgrad(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups,
                                      L.fold_mod, L.T, L.dgrad.ICs, L.dgrad.CoutW, L.E, c.s))
     return e;
@@ -519,6 +534,7 @@ int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float 
 // produced from the max-pool gradient).
 int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool_dP,
                 const int *pool_k, int training, int accumulate) {
+  tag(L.name, "bnbwd");
   const BNCoef coef = coef_at(c.sv, L.bn);
   const float *y = c.fptr(c.sv, L.y_off);
   const int64_t nvox = L.out.vox();
@@ -597,6 +613,7 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
+  tag(std::string("in"), "fwd");
   if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
   const float *src = xcl;
   const float *ssc = nullptr, *ssh = nullptr;
@@ -608,6 +625,7 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
     const BNCoef b2 = coef_at(c.sv, c2.bn);
     if (i < p.L - 1) {
       float *pp = c.fptr(c.sv, p.pool_off[i]);
+      tag(c2.name, "pool");
       if (int e = launch_maxpool_fwd(c.fptr(c.sv, c2.y_off), b2.scale, b2.shift, pp, p.B,
                                      c2.out.X, c2.out.Y, c2.out.Z, c2.out.Cs, s.pool_k[0],
                                      s.pool_k[1], s.pool_k[2], c.s))
@@ -622,6 +640,7 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   }
   for (int j = 0; j < p.L - 1; ++j) {
     const ConvTLayer &u = p.up[j];
+    tag(u.name, "fwd");
     float *U = c.fptr(c.sv, u.u_off);
     for (size_t ph = 0; ph < u.phases.size(); ++ph) {
       const int *pj = &u.pJ[ph * 6];
@@ -649,11 +668,13 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
     ssh = b2.shift;
   }
   const ConvLayer &last = p.L > 1 ? p.uc2[p.L - 2] : p.dc2[0];
+  tag(std::string("out"), "fwd");
   if (int e = launch_outconv_fwd(src, coef_at(c.sv, last.bn), c.P + p.oc_w, c.P + p.oc_b, t->out,
                                  p.B, last.out.vox() / p.B, last.out.C, last.out.Cs, p.Co, c.s))
     return e;
   if (training && t->bn_num_batches_tracked)
     if (int e = launch_bn_count_increment(t->bn_num_batches_tracked, p.n_bn, c.s)) return e;
+  if (timing_on()) timing_set_tag("");
   return HCU_OK;
 }
 
@@ -668,6 +689,7 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
 
   // out_conv + last BatchNorm
   const ConvLayer &last = p.uc2[p.L - 2];
+  tag(std::string("out"), "bwd");
   {
     const BNCoef coef = coef_at(c.sv, last.bn);
     const int64_t nvox = last.out.vox();
@@ -703,6 +725,7 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
     // conv1 (folded cat)
     if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, A, accumulate)) return e;
     // up_conv: bias, weight, input gradients (A holds dU)
+    tag(u.name, "wgrad");
     {
       const int R = chansum_rows(u.out.vox(), u.out.Cs);
       if (int e = launch_chansum(A, u.out.vox(), u.out.Cs, c.part(), R, c.s)) return e;
@@ -734,6 +757,7 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
       f.accumulate = accumulate;
       if (int e = launch_wgrad_finalize(f, c.s)) return e;
     }
+    tag(u.name, "dgrad");
     if (int e = launch_prep_convt_dgrad(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.T, u.dgrad.ICs,
                                         u.dgrad.CoutW, c.s))
       return e;
@@ -766,6 +790,7 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
       if (int e = launch_from_cl(A, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
     }
   }
+  if (timing_on()) timing_set_tag("");
   return HCU_OK;
 }
 

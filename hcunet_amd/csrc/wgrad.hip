@@ -105,7 +105,9 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
       const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
       for (int idx = tid; idx < HAV * CA4; idx += 256) {
         const int c4 = idx % CA4, v = idx / CA4;
-        const int hz = v % HAZ, q = v / HAZ, hy = q % a.HAY, hx = q / a.HAY;
+        int q, hz, hx, hy;
+        a.fHAZ.divmod(v, q, hz);
+        a.fHAY.divmod(q, hx, hy);
         const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
         const int c = ci0 + c4 * 4;
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -133,7 +135,9 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
       const int gx0 = px0 * a.gsx - a.gpx, gy0 = py0 * a.gsy - a.gpy, gz0 = pz0 * a.gsz - a.gpz;
       for (int idx = tid; idx < HGV * CG4; idx += 256) {
         const int c4 = idx % CG4, v = idx / CG4;
-        const int hz = v % HGZ, q = v / HGZ, hy = q % a.HGY, hx = q / a.HGY;
+        int q, hz, hx, hy;
+        a.fHGZ.divmod(v, q, hz);
+        a.fHGY.divmod(q, hx, hy);
         const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
         const int c = co0 + c4 * 4;
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -154,7 +158,9 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
       const int p = ks * 4 + (lane >> 4);
       const bool pv = p < PT;
       const int pp = pv ? p : 0;
-      const int lz = pp % a.TZ, q = pp / a.TZ, ly = q % a.TY, lx = q / a.TY;
+      int q, lz, lx, ly;
+      a.fTZ.divmod(pp, q, lz);
+      a.fTY.divmod(q, lx, ly);
       const int ah = lx * a.asx * HAYZ + ly * a.asy * HAZ + lz * a.asz;
       const int gh = lx * a.gsx * HGYZ + ly * a.gsy * HGZ + lz * a.gsz;
       float bv[NS];
@@ -301,6 +307,12 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
     txy = std::max(1, txy / 2);
   }
   if (a.lds_bytes > 65536) return fail(4, "wgrad: tile does not fit LDS");
+  a.fHAZ = FastDiv(a.HAZ);
+  a.fHAY = FastDiv(a.HAY);
+  a.fHGZ = FastDiv(a.HGZ);
+  a.fHGY = FastDiv(a.HGY);
+  a.fTZ = FastDiv(a.TZ);
+  a.fTY = FastDiv(a.TY);
   a.ntx = cdiv(a.PX, a.TX);
   a.nty = cdiv(a.PY, a.TY);
   a.ntz = ntz;
@@ -334,46 +346,63 @@ int launch_wgrad(const WGradArgs &a, hipStream_t s) {
   return 0;
 }
 
-__global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize f) {
+// Sum of the KB partial slabs per dW element, deterministic and parallel over
+// both the elements and the slabs: S threads share one element (each sums the
+// slabs k = s, s+S, ... in fp64), then the S sums are combined in LDS in a
+// fixed order.  The result is scattered into the PyTorch weight layout.
+__global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize f, int S) {
+  __shared__ double red[256];
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n;
-       idx += (int64_t)gridDim.x * 256) {
-    double s = 0.0;
-    for (int k = 0; k < f.KB; ++k) s += (double)f.partial[(size_t)k * n + idx];
-    const float v = (float)s;
-    const int grow = (int)(idx / f.Ntot), gcol = (int)(idx % f.Ntot);
-    if (f.mode == 0) {
-      const int o = gcol;
-      if (o >= f.Cout) continue;
-      if (grow == f.T * f.ACs) {
-        if (f.db) f.db[o] = f.accumulate ? f.db[o] + v : v;
-        continue;
-      }
-      const int t = grow / f.ACs, e = grow % f.ACs;
-      const int g = o / (f.Cout / f.groups);
-      const int cin_total = f.groups * f.Cin_g;
-      for (int cp = e; cp < cin_total; cp += f.fold_mod) {
-        const int c = cp - g * f.Cin_g;
-        if (c >= 0 && c < f.Cin_g) {
-          float *dst = f.dw + ((size_t)o * f.Cin_g + c) * f.T + t;
-          *dst = f.accumulate ? *dst + v : v;
-        }
-      }
-    } else {
-      const int ci = grow;
-      const int t = gcol / f.GCs, co = gcol % f.GCs;
-      if (ci >= f.Cin || co >= f.CoutT) continue;
-      float *dst = f.dw + ((size_t)ci * f.CoutT + co) * f.T + t;
-      *dst = f.accumulate ? *dst + v : v;
+  const int EPB = 256 / S;
+  const int tid = threadIdx.x, el = tid % EPB, sl = tid / EPB;
+  const int64_t idx = (int64_t)blockIdx.x * EPB + el;
+  double acc = 0.0;
+  if (idx < n) {
+    const float *src = f.partial + idx;
+#pragma unroll 4
+    for (int k = sl; k < f.KB; k += S) acc += (double)src[(size_t)k * n];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (sl != 0 || idx >= n) return;
+  double s = red[el];
+  for (int j = 1; j < S; ++j) s += red[j * EPB + el];
+  const float v = (float)s;
+  const int grow = (int)(idx / f.Ntot), gcol = (int)(idx % f.Ntot);
+  if (f.mode == 0) {
+    const int o = gcol;
+    if (o >= f.Cout) return;
+    if (grow == f.T * f.ACs) {
+      if (f.db) f.db[o] = f.accumulate ? f.db[o] + v : v;
+      return;
     }
+    const int t = grow / f.ACs, e = grow % f.ACs;
+    const int g = o / (f.Cout / f.groups);
+    const int cin_total = f.groups * f.Cin_g;
+    for (int cp = e; cp < cin_total; cp += f.fold_mod) {
+      const int c = cp - g * f.Cin_g;
+      if (c >= 0 && c < f.Cin_g) {
+        float *dst = f.dw + ((size_t)o * f.Cin_g + c) * f.T + t;
+        *dst = f.accumulate ? *dst + v : v;
+      }
+    }
+  } else {
+    const int ci = grow;
+    const int t = gcol / f.GCs, co = gcol % f.GCs;
+    if (ci >= f.Cin || co >= f.CoutT) return;
+    float *dst = f.dw + ((size_t)ci * f.CoutT + co) * f.T + t;
+    *dst = f.accumulate ? *dst + v : v;
   }
 }
 
 int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  int S = 1;
+  while (S < 64 && S * 2 <= f.KB && n * S / 256 < 1024) S *= 2;
+  const int EPB = 256 / S;
+  const int blocks = (int)((n + EPB - 1) / EPB);
   HCU_TIMED(s, "wgrad_finalize_kernel", 0.0, 4.0 * (double)n * (f.KB + 1),
-            hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f));
+            hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f, S));
   HCU_CHECK_LAUNCH();
   return 0;
 }

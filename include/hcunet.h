@@ -183,6 +183,8 @@ int hcu_maxpool_fwd_cl(int B, int C, int X, int Y, int Z, const int *k,
 /* ------------------------------------------------------------------------ */
 int hcu_timing_enable(int max_launches);
 int hcu_timing_disable(void);
+/* on != 0: report per network layer ("kernel@layer") instead of per symbol. */
+int hcu_timing_detail(int on);
 /* One line per kernel symbol: name\tcount\ttotal_ms\tflops\tbytes (totals
  * over launches; flops/bytes are algorithmic).  Returns bytes needed. */
 int64_t hcu_timing_report(char *buf, int64_t len);
