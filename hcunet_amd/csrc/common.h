@@ -76,12 +76,44 @@ struct GConvArgs {
   int CK, NSUB, MPW;
   int lds_bytes;
   FastDiv fHZ, fHY, fTZ, fTY;         // halo / tile index decomposition
+  // conv2 (conv2.hip): output-channel phases folded into N (ConvTranspose3d
+  // with kernel % stride == 0: n = phase*Cout + co, phase = (qx*phy+qy)*phz+qz
+  // stored at o*os + of + q), and the K split over channel chunks.
+  int nph, phx, phy, phz;
+  int ksplit, cps;                    // K-split count, channel chunks per split
+  size_t slice_floats;                // floats of one stored-tensor slice
+  float *partial;                     // [ksplit][stored tensor] when ksplit > 1
+  int use_conv2;
+  int NPF, gridx;                     // conv2 halo prefetch depth, persistent grid size
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 // Chooses the tile and kernel variant; returns 0 or an error code.
 int plan_gconv(GConvArgs &a, int target_blocks);
 int launch_gconv(const GConvArgs &a, hipStream_t s);
-inline int gconv_rows(const GConvArgs &a) { return a.B * a.ntx * a.nty * a.ntz; }
+int plan_conv2(GConvArgs &a, int target_blocks);
+int launch_conv2(const GConvArgs &a, hipStream_t s);
+size_t conv2_partial_floats(const GConvArgs &a);
+int conv2_stat_rows(const GConvArgs &a);
+// Plans conv2 when it supports the shape, else the generic gconv.
+bool conv2_disabled();   // HCU_NO_CONV2=1 forces the generic kernel (A/B testing)
+inline int plan_conv_any(GConvArgs &a, int target_blocks) {
+  GConvArgs b = a;
+  if (!conv2_disabled() && plan_conv2(b, target_blocks) == 0) {
+    a = b;
+    return 0;
+  }
+  a.use_conv2 = 0;
+  return plan_gconv(a, target_blocks);
+}
+inline int launch_conv_any(const GConvArgs &a, hipStream_t s) {
+  return a.use_conv2 ? launch_conv2(a, s) : launch_gconv(a, s);
+}
+inline int gconv_rows(const GConvArgs &a) {
+  return a.use_conv2 ? conv2_stat_rows(a) : a.B * a.ntx * a.nty * a.ntz;
+}
+inline size_t conv_partial_floats(const GConvArgs &a) {
+  return a.use_conv2 ? conv2_partial_floats(a) : 0;
+}
 
 // ---------------------------------------------------------------------------
 // Weight gradient (implicit GEMM, split over the reduction grid):
@@ -197,21 +229,68 @@ int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V,
                    hipStream_t s);
 
 // Weight preparation (PyTorch layout -> GEMM layouts).
+// Plain layout: wg[t][ci][co] (t < T, ci < ICs, co < CoutW).  Packed layout
+// for conv2 (on != 0): wg[chunk][s][g][co][j] with chunk = ci / CK, K-step s,
+// lane group g and component j as conv2_kernel consumes them (tap t =
+// s*TPS + g/(CK/4), ci = chunk*CK + 4*(g % (CK/4)) + j, TPS = 16/CK); taps
+// t >= T in the last step are zero.
+struct WPack {
+  int on, CK, S, ICs, CoutW;
+};
+inline WPack wpack_of(const GConvArgs &a) {
+  WPack p{};
+  if (!a.use_conv2) return p;
+  const int T = a.KX * a.KY * a.KZ, TPS = 16 / a.CK;
+  p.on = 1;
+  p.CK = a.CK;
+  p.S = (T + TPS - 1) / TPS;
+  p.ICs = a.ICs;
+  p.CoutW = a.CoutW;
+  return p;
+}
+// Floats of the prepared weight buffer of a GEMM planned in `a`.
+inline size_t wprep_floats(const GConvArgs &a) {
+  const int T = a.KX * a.KY * a.KZ;
+  if (!a.use_conv2) return (size_t)T * a.ICs * a.CoutW;
+  const WPack p = wpack_of(a);
+  return (size_t)a.ICs * p.S * (16 / p.CK) * a.CoutW;
+}
+// Packed index -> (t, ci, co); false for a padded tap.
+__device__ __forceinline__ bool wpack_decode(const WPack &p, int64_t i, int T, int &t, int &ci,
+                                             int &co) {
+  const int j = (int)(i & 3);
+  int64_t q = i >> 2;
+  co = (int)(q % p.CoutW);
+  q /= p.CoutW;
+  const int g = (int)(q & 3);
+  q >>= 2;
+  const int s = (int)(q % p.S);
+  const int chunk = (int)(q / p.S);
+  const int C4 = p.CK / 4, TPS = 4 / C4;
+  t = s * TPS + g / C4;
+  ci = chunk * p.CK + (g % C4) * 4 + j;
+  return t < T;
+}
 // Conv3d fwd:   wg[t][e][co] (e < ECs, co < CoutW)
 // Conv3d dgrad: wg[t'][co][e] (co < OCs, e < EW), t' = T-1-t
 int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int groups,
-                         int fold_mod, int T, int ECs, int CoutW, hipStream_t s);
+                         int fold_mod, int T, int ECs, int CoutW, WPack pk, hipStream_t s);
 int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g,
                            int groups, int fold_mod, int T, int OCs, int EW,
-                           int E, hipStream_t s);
+                           int E, WPack pk, hipStream_t s);
 // ConvTranspose3d fwd phase (px,py,pz): wg[t][ci][co], t over (Jx,Jy,Jz) taps
 int launch_prep_convt_fwd(const float *w, float *wg, int Cin, int Cout, int KX,
                           int KY, int KZ, int sx, int sy, int sz, int px, int py,
                           int pz, int Jx, int Jy, int Jz, int ICs, int CoutW,
                           hipStream_t s);
+// ConvTranspose3d fwd, all phases folded into N (kernel % stride == 0):
+// wg[t'][ci][ph*Cout + co], t' over (Jx,Jy,Jz) taps of the padded correlation.
+int launch_prep_convt_fused(const float *w, float *wg, int Cin, int Cout, int KX, int KY,
+                            int KZ, int sx, int sy, int sz, int ICs, int CoutW, WPack pk,
+                            hipStream_t s);
 // ConvTranspose3d dgrad: wg[t][co][ci] (co < UCs, ci < CinW)
 int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T,
-                            int UCs, int CinW, hipStream_t s);
+                            int UCs, int CinW, WPack pk, hipStream_t s);
 
 // Loss / optimizer (loss_adam.hip)
 int launch_loss_pixel(const float *pred, int B, int C, int PX, int PY, int PZ,

@@ -1,0 +1,591 @@
+// Implicit-GEMM convolution on fp32 MFMA (v_mfma_f32_16x16x4_f32), second
+// generation: channels-last LDS images read with ds_read_b128.
+//
+// GEMM view: M = output voxels of a TX*TY*TZ tile, N = output channels, K =
+// (tap, input channel).  One workgroup = 4 waves; wave w owns the 16-voxel
+// M-subtiles w, w+4, ... (MPW of them) and all NSUB*16 output channels of the
+// block.
+//
+// K ordering (a permutation of the reduction, so any order is exact): one
+// "step" covers 16 K-elements = (taps per step TPS) x CK channels, TPS = 16/CK.
+// Lane group g = lane/16 reads ONE ds_read_b128 = 4 consecutive channels
+// (c4 = g % (CK/4)) of its voxel shifted by tap t = s*TPS + g/(CK/4); component
+// j of that float4 feeds MFMA j.  The B fragment of lane (g, n) for MFMA j is
+// W[t][ci0 + 4*c4 + j][n], stored as one float4 in LDS, so each step is
+// 1 + NSUB b128 reads per (4 * NSUB) MFMAs per 16-voxel subtile.
+//
+// The input halo of the tile (BatchNorm+ReLU of the producer applied while
+// staging, zero outside the input) is staged channels-last as [hv][CKP]; the
+// block's weight slice as [s][g][NT][4].  Weights are read from the generic
+// prepared layout wg[t][ICs][CoutW] (prep_conv_* / prep_convt_*).
+//
+// K split: blockIdx.z selects a range of channel chunks; with ksplit > 1 the
+// raw partial sums go to `partial` ([ksplit][B][SX][SY][SZ][OCs]) and
+// conv2_reduce adds them (fixed order), the bias and the BatchNorm partial
+// statistics.
+//
+// Replaces the arithmetic of nn.Conv3d forward/input-gradient and
+// nn.ConvTranspose3d forward/input-gradient on the reference path
+// (hcat/unet.py:246-257, 281-298).
+#include "common.h"
+#include "timing.h"
+#include <algorithm>
+#include <cstdlib>
+
+namespace hcu {
+
+template <int CK, int NSUB, int MPW, int NPF>
+__global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NT = NSUB * 16;
+  constexpr int C4 = CK / 4;
+  constexpr int TPS = 4 / C4;          // taps per K-step
+  constexpr int CKP = CK + 4;          // padded channel stride of the halo image
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int T = a.KX * a.KY * a.KZ;
+  const int S = (T + TPS - 1) / TPS;
+  const int HZ = a.HZ, HYZ = a.HY * a.HZ;
+  const int HV = a.HX * HYZ;
+  const int nel = HV * C4;             // float4 elements of one halo image
+  float *alds = smem;                                  // [HV][CKP]
+  float *wlds = smem + ((HV * CKP + 3) & ~3);          // [S][4][NT][4]
+  int *toffs = reinterpret_cast<int *>(wlds + S * 4 * NT * 4);  // [S][4]
+  int *rowpk = toffs + S * 4;                                    // [MPW*64] (lx,ly,lz) of GEMM rows
+
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int n0 = blockIdx.y * NT;
+  const int MT = a.TX * a.TY * a.TZ;
+  const int nmsub = (MT + 15) >> 4;
+  const int nchunks = a.ICs / CK;
+  const int cb = blockIdx.z * a.cps, ce = min(nchunks, cb + a.cps);
+
+  // per-lane voxel offsets (halo coordinates) of the A rows: same for every tile
+  int vb[MPW];
+#pragma unroll
+  for (int j = 0; j < MPW; ++j) {
+    const int i = (wave + 4 * j) * 16 + r16;
+    int v = 0;
+    if (i < MT) {
+      int q, lz, lx, ly;
+      a.fTZ.divmod(i, q, lz);
+      a.fTY.divmod(q, lx, ly);
+      v = lx * a.sx * HYZ + ly * a.sy * HZ + lz * a.sz;
+    }
+    vb[j] = v * CKP;
+  }
+  for (int i = tid; i < MPW * 64; i += 256) {
+    int pk = -1;
+    if (i < MT) {
+      int q, lz, lx, ly;
+      a.fTZ.divmod(i, q, lz);
+      a.fTY.divmod(q, lx, ly);
+      pk = (lx << 20) | (ly << 10) | lz;
+    }
+    rowpk[i] = pk;
+  }
+  // tap offsets per (step, lane group); padded taps read voxel 0 (weights are 0)
+  for (int e = tid; e < S * 4; e += 256) {
+    const int t = (e >> 2) * TPS + (e & 3) / C4;
+    int off = 0;
+    if (t < T) {
+      const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
+      off = kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz;
+    }
+    toffs[e] = off * CKP + ((e & 3) % C4) * 4;
+  }
+
+  auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
+    b = tile / ntiles;
+    int r = tile - b * ntiles;
+    const int tzi = r % a.ntz;
+    r /= a.ntz;
+    const int tyi = r % a.nty;
+    const int txi = r / a.nty;
+    ox0 = txi * a.TX;
+    oy0 = tyi * a.TY;
+    oz0 = tzi * a.TZ;
+  };
+  // one halo element (float4 of 4 channels) of a tile, BN+ReLU applied; 0 outside
+  auto halo_elem = [&](int idx, int b, int gx0, int gy0, int gz0, int ci0) -> float4 {
+    float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int c4 = idx % C4;
+    const int v = idx / C4;
+    int t2, hz, hx, hy;
+    a.fHZ.divmod(v, t2, hz);
+    a.fHY.divmod(t2, hx, hy);
+    const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+    if ((unsigned)gx < (unsigned)a.IX && (unsigned)gy < (unsigned)a.IY &&
+        (unsigned)gz < (unsigned)a.IZ) {
+      const int c = ci0 + c4 * 4;
+      val = *reinterpret_cast<const float4 *>(
+          a.in + ((((size_t)b * a.IX + gx) * a.IY + gy) * a.IZ + gz) * a.ICs + c);
+      if (a.in_scale) {
+        const float4 sc = *reinterpret_cast<const float4 *>(a.in_scale + c);
+        const float4 sh = *reinterpret_cast<const float4 *>(a.in_shift + c);
+        val.x = fmaxf(fmaf(val.x, sc.x, sh.x), 0.f);
+        val.y = fmaxf(fmaf(val.y, sc.y, sh.y), 0.f);
+        val.z = fmaxf(fmaf(val.z, sc.z, sh.z), 0.f);
+        val.w = fmaxf(fmaf(val.w, sc.w, sh.w), 0.f);
+      }
+    }
+    return val;
+  };
+  auto halo_dst = [&](int idx) { return (idx / C4) * CKP + (idx % C4) * 4; };
+  // weight slice of one channel chunk: contiguous float4 copies from the packed layout
+  auto stage_w = [&](int chunk) {
+    const int n4 = S * 4 * NT;
+    const float4 *src = reinterpret_cast<const float4 *>(a.w);
+    for (int idx = tid; idx < n4; idx += 256) {
+      const int n = idx % NT, sg = idx / NT;
+      reinterpret_cast<float4 *>(wlds)[sg * NT + n] =
+          src[((size_t)chunk * S * 4 + sg) * a.CoutW + n0 + n];
+    }
+  };
+
+  floatx4 acc[MPW][NSUB];
+  // Subtiles past the tile (m >= nmsub) read voxel 0 and are never stored, so
+  // the step body has no per-subtile branch and the MFMA chains interleave.
+  auto compute = [&]() {
+    for (int s = 0; s < S; ++s) {
+      const int toff = toffs[s * 4 + g];
+      floatx4 bf[NSUB], av[MPW];
+#pragma unroll
+      for (int n = 0; n < NSUB; ++n)
+        bf[n] = *reinterpret_cast<const floatx4 *>(wlds + ((s * 4 + g) * NT + n * 16 + r16) * 4);
+#pragma unroll
+      for (int j = 0; j < MPW; ++j) av[j] = *reinterpret_cast<const floatx4 *>(alds + vb[j] + toff);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int j = 0; j < MPW; ++j)
+#pragma unroll
+          for (int n = 0; n < NSUB; ++n)
+            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][c], bf[n][c], acc[j][n], 0, 0, 0);
+    }
+  };
+
+  const bool split = a.ksplit > 1;
+  float *dst = split ? a.partial + (size_t)blockIdx.z * a.slice_floats : a.out;
+  // per-column store offset relative to the voxel (channel + output phase), or -1
+  float s1[NSUB], s2[NSUB], bias_v[NSUB];
+  int coff[NSUB];
+  bool cst[NSUB];
+#pragma unroll
+  for (int n = 0; n < NSUB; ++n) {
+    s1[n] = s2[n] = 0.f;
+    const int nn = n0 + n * 16 + r16;
+    bias_v[n] = (!split && a.bias && nn < a.Cout * a.nph) ? a.bias[nn % a.Cout] : 0.f;
+    int off = -1, co = nn;
+    if (a.nph > 1) {
+      if (nn < a.Cout * a.nph) {
+        const int ph = nn / a.Cout;
+        co = nn - ph * a.Cout;
+        const int qz = ph % a.phz, qq = ph / a.phz, qy = qq % a.phy, qx = qq / a.phy;
+        off = ((qx * a.SY + qy) * a.SZ + qz) * a.OCs + co;
+      }
+    } else if (nn < a.OCs) {
+      off = nn;   // padded channels < OCs are stored as 0
+    }
+    coff[n] = off;
+    cst[n] = off >= 0 && co < a.Cout;
+  }
+  const bool zpad = a.nph > 1 && a.OCs > a.Cout;
+  auto epilogue = [&](int b, int ox0, int oy0, int oz0) {
+#pragma unroll
+    for (int j = 0; j < MPW; ++j) {
+      const int m = wave + 4 * j;
+      if (m < nmsub) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int pk = rowpk[m * 16 + g * 4 + r];
+          if (pk >= 0) {
+            const int ox = ox0 + (pk >> 20), oy = oy0 + ((pk >> 10) & 1023), oz = oz0 + (pk & 1023);
+            if (ox < a.OX && oy < a.OY && oz < a.OZ) {
+              const size_t vbase = ((((size_t)b * a.SX + ox * a.osx + a.ofx) * a.SY +
+                                     oy * a.osy + a.ofy) * a.SZ + oz * a.osz + a.ofz) * a.OCs;
+#pragma unroll
+              for (int n = 0; n < NSUB; ++n) {
+                if (coff[n] < 0) continue;
+                const float val = acc[j][n][r] + bias_v[n];
+                dst[vbase + coff[n]] = val;
+                if (cst[n]) {
+                  s1[n] += val;
+                  s2[n] = fmaf(val, val, s2[n]);
+                }
+              }
+              if (zpad) {   // ConvTranspose3d phases: zero the padded channels of U
+#pragma unroll
+                for (int n = 0; n < NSUB; ++n) {
+                  const int nn = n0 + n * 16 + r16;
+                  if (coff[n] >= 0 && nn % a.Cout == a.Cout - 1)
+                    for (int cz = 1; cz <= a.OCs - a.Cout; ++cz) dst[vbase + coff[n] + cz] = 0.f;
+                }
+              }
+            }
+          }
+        }
+      }
+    }
+  };
+
+  if (NPF > 0 && ce - cb == 1) {
+    // ---- single channel chunk: weights staged once, next tile's halo in flight.
+    // Thread tid always handles channel group c4 = tid % C4 of halo voxels
+    // v = tid / C4 + u * (256 / C4); their halo coordinates are fixed per launch.
+    constexpr int VS = 256 / C4;
+    stage_w(cb);
+    const int ci0 = cb * CK;
+    const int c4 = tid % C4, c = ci0 + c4 * 4;
+    float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool act = a.in_scale != nullptr;
+    if (act) {
+      sc = *reinterpret_cast<const float4 *>(a.in_scale + c);
+      sh = *reinterpret_cast<const float4 *>(a.in_shift + c);
+    }
+    int hpk[NPF > 0 ? NPF : 1], goff[NPF > 0 ? NPF : 1];
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int v = tid / C4 + u * VS;
+      hpk[u] = -1;
+      goff[u] = 0;
+      if (v < HV) {
+        int t2, hz, hx, hy;
+        a.fHZ.divmod(v, t2, hz);
+        a.fHY.divmod(t2, hx, hy);
+        hpk[u] = (hx << 20) | (hy << 10) | hz;
+        goff[u] = ((hx * a.IY + hy) * a.IZ + hz) * a.ICs;
+      }
+    }
+    const int dst0 = (tid / C4) * CKP + c4 * 4;
+    float4 pf[NPF > 0 ? NPF : 1];
+    auto load_tile = [&](int tile) {
+      int b, x0, y0, z0;
+      tile_origin(tile, b, x0, y0, z0);
+      const int gx0 = x0 * a.sx - a.px, gy0 = y0 * a.sy - a.py, gz0 = z0 * a.sz - a.pz;
+      const int64_t base = ((((int64_t)b * a.IX + gx0) * a.IY + gy0) * a.IZ + gz0) * a.ICs + c;
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int hp = hpk[u];
+        if (hp >= 0) {
+          const int gx = gx0 + (hp >> 20), gy = gy0 + ((hp >> 10) & 1023), gz = gz0 + (hp & 1023);
+          if ((unsigned)gx < (unsigned)a.IX && (unsigned)gy < (unsigned)a.IY &&
+              (unsigned)gz < (unsigned)a.IZ) {
+            val = *reinterpret_cast<const float4 *>(a.in + base + goff[u]);
+            if (act) {
+              val.x = fmaxf(fmaf(val.x, sc.x, sh.x), 0.f);
+              val.y = fmaxf(fmaf(val.y, sc.y, sh.y), 0.f);
+              val.z = fmaxf(fmaf(val.z, sc.z, sh.z), 0.f);
+              val.w = fmaxf(fmaf(val.w, sc.w, sh.w), 0.f);
+            }
+          }
+        }
+        pf[u] = val;
+      }
+    };
+    int tile = blockIdx.x;
+    if (tile < total) load_tile(tile);
+    for (; tile < total; tile += gridDim.x) {
+      int b, ox0, oy0, oz0;
+      tile_origin(tile, b, ox0, oy0, oz0);
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < NPF; ++u)
+        if (hpk[u] >= 0) *reinterpret_cast<float4 *>(alds + dst0 + u * VS * CKP) = pf[u];
+      __syncthreads();
+      if (tile + (int)gridDim.x < total) load_tile(tile + gridDim.x);
+#pragma unroll
+      for (int j = 0; j < MPW; ++j)
+#pragma unroll
+        for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      compute();
+      epilogue(b, ox0, oy0, oz0);
+    }
+  } else {
+    for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
+      int b, ox0, oy0, oz0;
+      tile_origin(tile, b, ox0, oy0, oz0);
+      const int gx0 = ox0 * a.sx - a.px, gy0 = oy0 * a.sy - a.py, gz0 = oz0 * a.sz - a.pz;
+#pragma unroll
+      for (int j = 0; j < MPW; ++j)
+#pragma unroll
+        for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int chunk = cb; chunk < ce; ++chunk) {
+        const int ci0 = chunk * CK;
+        __syncthreads();
+        for (int base = tid; base < nel; base += 4 * 256) {
+          float4 val[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * 256;
+            val[u] = idx < nel ? halo_elem(idx, b, gx0, gy0, gz0, ci0) : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int idx = base + u * 256;
+            if (idx < nel) *reinterpret_cast<float4 *>(alds + halo_dst(idx)) = val[u];
+          }
+        }
+        stage_w(chunk);
+        __syncthreads();
+        compute();
+      }
+      epilogue(b, ox0, oy0, oz0);
+    }
+  }
+
+  if (a.stats && !split) {
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) {
+      s1[n] += __shfl_xor(s1[n], 16);
+      s1[n] += __shfl_xor(s1[n], 32);
+      s2[n] += __shfl_xor(s2[n], 16);
+      s2[n] += __shfl_xor(s2[n], 32);
+    }
+    __syncthreads();
+    float *red = smem;  // [4][NT][2]
+    if (lane < 16) {
+#pragma unroll
+      for (int n = 0; n < NSUB; ++n) {
+        red[(wave * NT + n * 16 + lane) * 2 + 0] = s1[n];
+        red[(wave * NT + n * 16 + lane) * 2 + 1] = s2[n];
+      }
+    }
+    __syncthreads();
+    if (tid < NT) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        t1 += red[(w * NT + tid) * 2 + 0];
+        t2 += red[(w * NT + tid) * 2 + 1];
+      }
+      const size_t row = blockIdx.x;
+      a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
+      a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+    }
+  }
+}
+
+// Sum of the K-split partial slices in a fixed order, + bias, store, and the
+// BatchNorm partial statistics of each block's rows (one stats row per block).
+// Every element of the stored tensor [B][SX][SY][SZ][OCs] is produced by
+// exactly one (voxel, channel) of the GEMM, so the slices are fully written.
+// Requires 256 % (OCs/4) == 0 (plan_conv2 only splits such layers).
+__global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, int vox_per_block) {
+  __shared__ float red[256][2];
+  const int64_t nvox = (int64_t)a.B * a.SX * a.SY * a.SZ;
+  const int C4 = a.OCs / 4;
+  const int tid = threadIdx.x;
+  const int c4 = tid % C4;
+  const int vstep = 256 / C4;
+  const int64_t v0 = (int64_t)blockIdx.x * vox_per_block;
+  const int64_t v1 = min(v0 + vox_per_block, nvox);
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.bias) {
+    const int c = c4 * 4;
+    bv.x = c + 0 < a.Cout ? a.bias[c + 0] : 0.f;
+    bv.y = c + 1 < a.Cout ? a.bias[c + 1] : 0.f;
+    bv.z = c + 2 < a.Cout ? a.bias[c + 2] : 0.f;
+    bv.w = c + 3 < a.Cout ? a.bias[c + 3] : 0.f;
+  }
+  float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t v = v0 + tid / C4; v < v1; v += vstep) {
+    const size_t off = (size_t)v * a.OCs + c4 * 4;
+    float4 s = *reinterpret_cast<const float4 *>(a.partial + off);
+    for (int k = 1; k < a.ksplit; ++k) {
+      const float4 p = *reinterpret_cast<const float4 *>(a.partial + (size_t)k * a.slice_floats + off);
+      s.x += p.x;
+      s.y += p.y;
+      s.z += p.z;
+      s.w += p.w;
+    }
+    s.x += bv.x;
+    s.y += bv.y;
+    s.z += bv.z;
+    s.w += bv.w;
+    *reinterpret_cast<float4 *>(a.out + off) = s;
+    st1[0] += s.x; st1[1] += s.y; st1[2] += s.z; st1[3] += s.w;
+    st2[0] = fmaf(s.x, s.x, st2[0]);
+    st2[1] = fmaf(s.y, s.y, st2[1]);
+    st2[2] = fmaf(s.z, s.z, st2[2]);
+    st2[3] = fmaf(s.w, s.w, st2[3]);
+  }
+  if (!a.stats) return;
+  for (int comp = 0; comp < 4; ++comp) {
+    __syncthreads();
+    red[tid][0] = st1[comp];
+    red[tid][1] = st2[comp];
+    __syncthreads();
+    if (tid < C4) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = tid; k < 256; k += C4) {
+        t1 += red[k][0];
+        t2 += red[k][1];
+      }
+      const int c = tid * 4 + comp;
+      a.stats[((size_t)blockIdx.x * a.CoutW + c) * 2 + 0] = t1;
+      a.stats[((size_t)blockIdx.x * a.CoutW + c) * 2 + 1] = t2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+bool conv2_disabled() {
+  static const bool off = [] {
+    const char *e = getenv("HCU_NO_CONV2");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
+static void tile2(int OX, int OY, int TZ, int maxM, int &TX, int &TY) {
+  const int txy = std::max(1, maxM / TZ);
+  TX = 1;
+  while ((TX + 1) * (TX + 1) <= txy) ++TX;
+  TY = std::max(1, txy / TX);
+  if (TX > OX) { TX = OX; TY = std::max(1, std::min(OY, txy / TX)); }
+  if (TY > OY) { TY = OY; TX = std::max(1, std::min(OX, txy / TY)); }
+}
+
+static long conv2_lds(const GConvArgs &a, int CK, int NT) {
+  const int T = a.KX * a.KY * a.KZ;
+  const int TPS = 16 / CK;
+  const int S = (T + TPS - 1) / TPS;
+  const long HV = (long)a.HX * a.HY * a.HZ;
+  return (((HV * (CK + 4) + 3) & ~3L) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 64) * 4;
+}
+
+// Chooses CK / NSUB / MPW / tile / K split / prefetch depth / grid for
+// conv2_kernel.  Returns 0, or a non-zero code when conv2 cannot run this
+// shape (the caller then keeps gconv).
+int plan_conv2(GConvArgs &a, int target_blocks) {
+  if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return fail(2, "conv2: empty output grid");
+  if (a.ICs % 4 != 0 || a.OCs % 4 != 0) return fail(1, "conv2: channel strides must be multiples of 4");
+  if (a.nph < 1) a.nph = 1;
+  if (a.phx < 1) a.phx = 1;
+  if (a.phy < 1) a.phy = 1;
+  if (a.phz < 1) a.phz = 1;
+  const int Nlog = a.Cout * a.nph;
+  const int nb16 = cdiv(Nlog, 16);
+  a.NSUB = nb16 >= 3 ? 4 : nb16;
+  const int NT = a.NSUB * 16;
+  a.CoutW = round_up(Nlog, NT);
+  const int ntz = cdiv(a.OZ, 16);
+  a.TZ = cdiv(a.OZ, ntz);
+  const int nN = a.CoutW / NT;
+  // MPW: largest tile that still gives enough tiles to fill the chip
+  const int mpws[3] = {4, 2, 1};
+  for (int mi = 0; mi < 3; ++mi) {
+    const int MPW = mpws[mi];
+    int TX, TY;
+    tile2(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
+    const long blocks = (long)cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz * nN * a.B;
+    a.MPW = MPW;
+    a.TX = TX;
+    a.TY = TY;
+    if (blocks >= target_blocks) break;
+  }
+  a.ntx = cdiv(a.OX, a.TX);
+  a.nty = cdiv(a.OY, a.TY);
+  a.ntz = ntz;
+  a.HX = (a.TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
+  a.HY = (a.TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
+  a.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
+  a.CK = 0;
+  const int cks[3] = {16, 8, 4};
+  for (int i = 0; i < 3; ++i) {
+    const int CK = cks[i];
+    if (a.ICs % CK) continue;
+    const long lds = conv2_lds(a, CK, NT);
+    if (lds <= 56 * 1024) {
+      a.CK = CK;
+      a.lds_bytes = (int)lds;
+      break;
+    }
+  }
+  if (!a.CK) return fail(4, "conv2: no tile fits in LDS");
+  if (a.lds_bytes < 4 * NT * 2 * 4) a.lds_bytes = 4 * NT * 2 * 4;
+  const long tiles = (long)a.ntx * a.nty * a.ntz * a.B;
+  const int nchunks = a.ICs / a.CK;
+  int ks = 1;
+  if (256 % (a.OCs / 4) == 0)
+    while (ks < nchunks && tiles * nN * ks < target_blocks) ks *= 2;
+  ks = std::min(ks, nchunks);
+  a.cps = cdiv(nchunks, ks);
+  a.ksplit = cdiv(nchunks, a.cps);
+  a.slice_floats = (size_t)a.B * a.SX * a.SY * a.SZ * a.OCs;
+  // halo prefetch depth (float4 per thread) for single-chunk blocks
+  const long nel = (long)a.HX * a.HY * a.HZ * (a.CK / 4);
+  a.NPF = 0;
+  if (a.cps == 1) {
+    if (nel <= 4 * 256) a.NPF = 4;
+    else if (nel <= 8 * 256) a.NPF = 8;
+  }
+  // persistent grid: up to `occ` resident blocks per CU
+  const int occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
+  const long slots = (long)256 * occ;
+  const long per_tile = (long)nN * a.ksplit;
+  long gx = std::max(1L, slots / per_tile);
+  a.gridx = (int)std::min(tiles, gx);
+  a.fHZ = FastDiv(a.HZ);
+  a.fHY = FastDiv(a.HY);
+  a.fTZ = FastDiv(a.TZ);
+  a.fTY = FastDiv(a.TY);
+  a.use_conv2 = 1;
+  return 0;
+}
+
+size_t conv2_partial_floats(const GConvArgs &a) {
+  return a.ksplit > 1 ? (size_t)a.ksplit * a.slice_floats : 0;
+}
+
+static int reduce_vox_per_block(const GConvArgs &a) { return 2 * 256 / (a.OCs / 4); }
+
+int conv2_stat_rows(const GConvArgs &a) {
+  if (a.ksplit > 1) {
+    const int64_t nvox = (int64_t)a.B * a.SX * a.SY * a.SZ;
+    const int vpb = reduce_vox_per_block(a);
+    return (int)((nvox + vpb - 1) / vpb);
+  }
+  return a.gridx;
+}
+
+#define CONV2_CASE(CK_, NS_, MP_, PF_)                                                         \
+  if (a.CK == CK_ && a.NSUB == NS_ && a.MPW == MP_ && a.NPF == PF_) {                           \
+    HCU_TIMED(s, "conv2_kernel<" #CK_ "," #NS_ "," #MP_ "," #PF_ ">", fl, by,                     \
+              hipLaunchKernelGGL((conv2_kernel<CK_, NS_, MP_, PF_>), grid, dim3(256),           \
+                                 a.lds_bytes, s, a));                                           \
+    launched = true;                                                                            \
+  }
+#define CONV2_PF(CK_, NS_, MP_) \
+  CONV2_CASE(CK_, NS_, MP_, 0) else CONV2_CASE(CK_, NS_, MP_, 4) else CONV2_CASE(CK_, NS_, MP_, 8)
+#define CONV2_MP(CK_, NS_) CONV2_PF(CK_, NS_, 1) else CONV2_PF(CK_, NS_, 2) else CONV2_PF(CK_, NS_, 4)
+#define CONV2_NS(CK_) CONV2_MP(CK_, 1) else CONV2_MP(CK_, 2) else CONV2_MP(CK_, 4)
+
+int launch_conv2(const GConvArgs &a, hipStream_t s) {
+  const dim3 grid(a.gridx, a.CoutW / (a.NSUB * 16), a.ksplit);
+  if (grid.y > 65535 || grid.z > 65535) return fail(4, "conv2: grid too large");
+  if (a.ksplit > 1 && !a.partial) return fail(5, "conv2: K split needs a partial workspace");
+  const double fl = a.flops > 0 ? a.flops
+                                : 2.0 * a.B * a.OX * a.OY * a.OZ * (double)a.Cout * a.nph * a.KX *
+                                      a.KY * a.KZ * a.ICs;
+  const double by = 4.0 * ((double)a.B * a.IX * a.IY * a.IZ * a.ICs +
+                           (double)a.B * a.SX * a.SY * a.SZ * a.OCs);
+  bool launched = false;
+  CONV2_NS(4) else CONV2_NS(8) else CONV2_NS(16)
+  if (!launched) return fail(4, "conv2: unsupported variant");
+  HCU_CHECK_LAUNCH();
+  if (a.ksplit > 1) {
+    const int64_t nvox = (int64_t)a.B * a.SX * a.SY * a.SZ;
+    const int vpb = reduce_vox_per_block(a);
+    const int blocks = (int)((nvox + vpb - 1) / vpb);
+    HCU_TIMED(s, "conv2_reduce_kernel", 0.0, 4.0 * (double)(a.ksplit + 1) * a.slice_floats,
+              hipLaunchKernelGGL(conv2_reduce_kernel, dim3(blocks), dim3(256), 0, s, a, vpb));
+    HCU_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace hcu

@@ -635,51 +635,64 @@ __device__ inline float weff(const float *w, int o, int e, int t, int Cout, int 
   return s;
 }
 
+__device__ __forceinline__ int64_t prep_count(const WPack &pk, int T, int ICs, int CoutW) {
+  return pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * ICs * CoutW;
+}
+// (t, ci, co) of element i of the prepared buffer (plain or packed layout).
+__device__ __forceinline__ bool prep_index(const WPack &pk, int64_t i, int T, int ICs, int CoutW,
+                                           int &t, int &ci, int &co) {
+  if (pk.on) return wpack_decode(pk, i, T, t, ci, co);
+  co = (int)(i % CoutW);
+  const int64_t q = i / CoutW;
+  ci = (int)(q % ICs);
+  t = (int)(q / ICs);
+  return true;
+}
+
 __global__ void __launch_bounds__(256)
 prep_conv_fwd_kernel(const float *w, float *wg, int Cout, int Cin_g, int groups,
-                     int fold_mod, int T, int ECs, int CoutW, int E) {
-  const int64_t n = (int64_t)T * ECs * CoutW;
+                     int fold_mod, int T, int ECs, int CoutW, int E, WPack pk) {
+  const int64_t n = prep_count(pk, T, ECs, CoutW);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
-    const int co = (int)(i % CoutW);
-    const int64_t q = i / CoutW;
-    const int e = (int)(q % ECs);
-    const int t = (int)(q / ECs);
-    wg[i] = (co < Cout && e < E) ? weff(w, co, e, t, Cout, Cin_g, groups, fold_mod, T) : 0.f;
+    int t, e, co;
+    float v = 0.f;
+    if (prep_index(pk, i, T, ECs, CoutW, t, e, co) && co < Cout && e < E)
+      v = weff(w, co, e, t, Cout, Cin_g, groups, fold_mod, T);
+    wg[i] = v;
   }
 }
 
 int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int groups,
-                         int fold_mod, int T, int ECs, int CoutW, hipStream_t s) {
+                         int fold_mod, int T, int ECs, int CoutW, WPack pk, hipStream_t s) {
   const int E = std::min(fold_mod, groups * Cin_g);
-  const int64_t n = (int64_t)T * ECs * CoutW;
+  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * ECs * CoutW;
   HCU_TIMED(s, "prep_conv_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
-                     Cin_g, groups, fold_mod, T, ECs, CoutW, E));
+                     Cin_g, groups, fold_mod, T, ECs, CoutW, E, pk));
   HCU_CHECK_LAUNCH();
   return 0;
 }
 
+// dgrad GEMM: rows (ci of the GEMM) = conv output channels co, cols = input channels e.
 __global__ void __launch_bounds__(256)
 prep_conv_dgrad_kernel(const float *w, float *wg, int Cout, int Cin_g, int groups,
-                       int fold_mod, int T, int OCs, int EW, int E) {
-  const int64_t n = (int64_t)T * OCs * EW;
+                       int fold_mod, int T, int OCs, int EW, int E, WPack pk) {
+  const int64_t n = prep_count(pk, T, OCs, EW);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
-    const int e = (int)(i % EW);
-    const int64_t q = i / EW;
-    const int co = (int)(q % OCs);
-    const int tp = (int)(q / OCs);
-    wg[i] = (co < Cout && e < E)
-                ? weff(w, co, e, T - 1 - tp, Cout, Cin_g, groups, fold_mod, T)
-                : 0.f;
+    int tp, co, e;
+    float v = 0.f;
+    if (prep_index(pk, i, T, OCs, EW, tp, co, e) && co < Cout && e < E)
+      v = weff(w, co, e, T - 1 - tp, Cout, Cin_g, groups, fold_mod, T);
+    wg[i] = v;
   }
 }
 
 int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g, int groups,
-                           int fold_mod, int T, int OCs, int EW, int E, hipStream_t s) {
-  const int64_t n = (int64_t)T * OCs * EW;
+                           int fold_mod, int T, int OCs, int EW, int E, WPack pk, hipStream_t s) {
+  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * OCs * EW;
   HCU_TIMED(s, "prep_conv_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
-                     Cin_g, groups, fold_mod, T, OCs, EW, E));
+                     Cin_g, groups, fold_mod, T, OCs, EW, E, pk));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -717,24 +730,59 @@ int launch_prep_convt_fwd(const float *w, float *wg, int Cin, int Cout, int KX, 
 }
 
 __global__ void __launch_bounds__(256)
-prep_convt_dgrad_kernel(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
-                        int CinW) {
-  const int64_t n = (int64_t)T * UCs * CinW;
+prep_convt_fused_kernel(const float *w, float *wg, int Cin, int Cout, int KX, int KY, int KZ,
+                        int sx, int sy, int sz, int ICs, int CoutW, WPack pk) {
+  const int Jx = KX / sx, Jy = KY / sy, Jz = KZ / sz;
+  const int T = Jx * Jy * Jz;
+  const int nph = sx * sy * sz;
+  const int64_t n = prep_count(pk, T, ICs, CoutW);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
-    const int ci = (int)(i % CinW);
-    const int64_t q = i / CinW;
-    const int co = (int)(q % UCs);
-    const int t = (int)(q / UCs);
-    wg[i] = (ci < Cin && co < Cout) ? w[((size_t)ci * Cout + co) * T + t] : 0.f;
+    int t, ci, nn;
+    float v = 0.f;
+    if (prep_index(pk, i, T, ICs, CoutW, t, ci, nn) && ci < Cin && nn < nph * Cout) {
+      const int ph = nn / Cout, co = nn % Cout;
+      const int qz = ph % sz, qy = (ph / sz) % sy, qx = ph / (sz * sy);
+      const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
+      const int kx = qx + sx * (Jx - 1 - tx), ky = qy + sy * (Jy - 1 - ty),
+                kz = qz + sz * (Jz - 1 - tz);
+      v = w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
+    }
+    wg[i] = v;
+  }
+}
+
+int launch_prep_convt_fused(const float *w, float *wg, int Cin, int Cout, int KX, int KY,
+                            int KZ, int sx, int sy, int sz, int ICs, int CoutW, WPack pk,
+                            hipStream_t s) {
+  const int T = (KX / sx) * (KY / sy) * (KZ / sz);
+  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * ICs * CoutW;
+  HCU_TIMED(s, "prep_convt_fused_kernel", 0.0, 0.0,
+            hipLaunchKernelGGL(prep_convt_fused_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg,
+                               Cin, Cout, KX, KY, KZ, sx, sy, sz, ICs, CoutW, pk));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void __launch_bounds__(256)
+prep_convt_dgrad_kernel(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
+                        int CinW, WPack pk) {
+  const int64_t n = prep_count(pk, T, UCs, CinW);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    int t, co, ci;
+    float v = 0.f;
+    if (prep_index(pk, i, T, UCs, CinW, t, co, ci) && ci < Cin && co < Cout)
+      v = w[((size_t)ci * Cout + co) * T + t];
+    wg[i] = v;
   }
 }
 
 int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
-                            int CinW, hipStream_t s) {
-  const int64_t n = (int64_t)T * UCs * CinW;
+                            int CinW, WPack pk, hipStream_t s) {
+  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * UCs * CinW;
   HCU_TIMED(s, "prep_convt_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
-                     Cout, T, UCs, CinW));
+                     Cout, T, UCs, CinW, pk));
   HCU_CHECK_LAUNCH();
   return 0;
 }

@@ -97,6 +97,8 @@ struct ConvTLayer {
   Dims in, out;
   std::vector<GConvArgs> phases;
   std::vector<int> pJ;  // 6 ints per phase: px,py,pz,Jx,Jy,Jz
+  bool fused = false;   // kernel % stride == 0: all phases in one GEMM (N = phase x Cout)
+  GConvArgs fwdf{};
   GConvArgs dgrad{};
   WGradArgs wg{};
   size_t u_off = 0;
@@ -180,9 +182,9 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
                                    "). Kernel size can't be greater than actual input size");
   L.out = mkdims(in.B, ox, oy, oz, Cout);
   L.fwd = gconv_conv_fwd(in, L.out, K, D, Cout);
-  if (int e = plan_gconv(L.fwd, kTargetBlocks)) return e;
+  if (int e = plan_conv_any(L.fwd, kTargetBlocks)) return e;
   L.dgrad = gconv_conv_dgrad(in, L.out, K, D, L.E);
-  if (int e = plan_gconv(L.dgrad, kTargetBlocks)) return e;
+  if (int e = plan_conv_any(L.dgrad, kTargetBlocks)) return e;
   L.wg = wgrad_conv(in, L.out, K, D);
   if (int e = plan_wgrad(L.wg, kTargetBlocks)) return e;
   L.bn.C = Cout;
@@ -193,7 +195,7 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
 
 
 int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int S[3],
-                size_t &max_wprep, size_t &max_part) {
+                size_t &max_wprep, size_t &max_part, size_t &max_kpart) {
   const int f = cur.C;
   u.Cin = f;
   u.Cout = o;
@@ -210,6 +212,28 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
   u.phases.clear();
   u.pJ.clear();
   const int nph = u.S[0] * u.S[1] * u.S[2];
+  u.fused = u.K[0] % u.S[0] == 0 && u.K[1] % u.S[1] == 0 && u.K[2] % u.S[2] == 0;
+  if (u.fused) {
+    const int Jx = u.K[0] / u.S[0], Jy = u.K[1] / u.S[1], Jz = u.K[2] / u.S[2];
+    GConvArgs a{};
+    a.B = cur.B;
+    a.IX = cur.X; a.IY = cur.Y; a.IZ = cur.Z; a.ICs = cur.Cs;
+    a.OX = cur.X + Jx - 1; a.OY = cur.Y + Jy - 1; a.OZ = cur.Z + Jz - 1;
+    a.SX = ux; a.SY = uy; a.SZ = uz; a.OCs = u.out.Cs; a.Cout = o;
+    a.osx = u.S[0]; a.osy = u.S[1]; a.osz = u.S[2];
+    a.KX = Jx; a.KY = Jy; a.KZ = Jz;
+    a.sx = a.sy = a.sz = 1;
+    a.dx = a.dy = a.dz = 1;
+    a.px = Jx - 1; a.py = Jy - 1; a.pz = Jz - 1;
+    a.nph = nph; a.phx = u.S[0]; a.phy = u.S[1]; a.phz = u.S[2];
+    if (plan_conv2(a, kTargetBlocks) == 0) {
+      u.fwdf = a;
+      max_wprep = std::max(max_wprep, wprep_floats(a));
+      max_kpart = std::max(max_kpart, conv_partial_floats(a));
+    } else {
+      u.fused = false;
+    }
+  }
   for (int qx = 0; qx < u.S[0]; ++qx)
     for (int qy = 0; qy < u.S[1]; ++qy)
       for (int qz = 0; qz < u.S[2]; ++qz) {
@@ -244,9 +268,10 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     a.KX = u.K[0]; a.KY = u.K[1]; a.KZ = u.K[2];
     a.sx = u.S[0]; a.sy = u.S[1]; a.sz = u.S[2];
     a.dx = a.dy = a.dz = 1;
-    if (int e = plan_gconv(a, kTargetBlocks)) return e;
+    if (int e = plan_conv_any(a, kTargetBlocks)) return e;
     u.dgrad = a;
-    max_wprep = std::max(max_wprep, (size_t)u.T * a.ICs * a.CoutW);
+    max_wprep = std::max(max_wprep, wprep_floats(a));
+    max_kpart = std::max(max_kpart, conv_partial_floats(a));
   }
   {  // wgrad: rows = ci, cols = (t, co)
     WGradArgs w{};
@@ -287,14 +312,14 @@ struct hcu_unet_plan {
   size_t saved_bytes = 0, scratch_bytes = 0;
   // scratch layout
   size_t buf_off[2] = {0, 0};
-  size_t part_off = 0, wprep_off = 0;
-  size_t max_act = 0, max_part = 0, max_wprep = 0;
+  size_t part_off = 0, wprep_off = 0, kpart_off = 0;
+  size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
 };
 
 namespace {
 
-size_t prep_floats_fwd(const ConvLayer &L) { return (size_t)L.T * L.fwd.ICs * L.fwd.CoutW; }
-size_t prep_floats_dgrad(const ConvLayer &L) { return (size_t)L.T * L.dgrad.ICs * L.dgrad.CoutW; }
+size_t prep_floats_fwd(const ConvLayer &L) { return wprep_floats(L.fwd); }
+size_t prep_floats_dgrad(const ConvLayer &L) { return wprep_floats(L.dgrad); }
 
 void track_conv(hcu_unet_plan &p, const ConvLayer &L) {
   p.max_act = std::max(p.max_act, std::max(L.in.floats(), L.out.floats()));
@@ -302,6 +327,7 @@ void track_conv(hcu_unet_plan &p, const ConvLayer &L) {
   p.max_part = std::max(p.max_part, wgrad_partial_floats(L.wg));
   p.max_part = std::max(p.max_part, (size_t)bwd_rows(L.out.vox(), L.out.Cs) * L.out.Cs * 2);
   p.max_wprep = std::max(p.max_wprep, std::max(prep_floats_fwd(L), prep_floats_dgrad(L)));
+  p.max_kpart = std::max(p.max_kpart, std::max(conv_partial_floats(L.fwd), conv_partial_floats(L.dgrad)));
 }
 
 int build_plan(hcu_unet_plan &p) {
@@ -412,7 +438,7 @@ int build_plan(hcu_unet_plan &p) {
     const int level = L - 2 - j;
     const int f = s.features[L - 1 - j], o = s.features[L - 2 - j];
     ConvTLayer &u = p.up[j];
-    if (int e = setup_convt(u, cur, o, s.up_k, s.up_s, p.max_wprep, p.max_part)) return e;
+    if (int e = setup_convt(u, cur, o, s.up_k, s.up_s, p.max_wprep, p.max_part, p.max_kpart)) return e;
     const Dims &skip = p.dc2[level].out;
     if (u.out.X > skip.X || u.out.Y > skip.Y || u.out.Z > skip.Z)
       return fail(HCU_ERR_SHAPE,
@@ -445,6 +471,7 @@ int build_plan(hcu_unet_plan &p) {
   p.buf_off[1] = scratch.take_floats(p.max_act);
   p.part_off = scratch.take_floats(p.max_part);
   p.wprep_off = scratch.take_floats(p.max_wprep);
+  p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
   p.scratch_bytes = scratch.off;
   return 0;
 }
@@ -460,6 +487,7 @@ struct Ctx {
   float *part() const { return fptr(sc, p.part_off); }
   float *wprep() const { return fptr(sc, p.wprep_off); }
   float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
+  float *kpart() const { return fptr(sc, p.kpart_off); }
 };
 
 void tag(const std::string &layer, const char *phase) {
@@ -471,7 +499,7 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   HCU_HIP(hipGetLastError());
   tag(L.name, "fwd");
   if (int e = launch_prep_conv_fwd(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups, L.fold_mod,
-                                   L.T, L.fwd.ICs, L.fwd.CoutW, c.s))
+                                   L.T, L.fwd.ICs, L.fwd.CoutW, wpack_of(L.fwd), c.s))
     return e;
   GConvArgs a = L.fwd;
   a.in = in;
@@ -481,7 +509,8 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   a.bias = c.P + L.b_off;
   a.out = c.fptr(c.sv, L.y_off);
   a.stats = training ? c.part() : nullptr;
-  if (int e = launch_gconv(a, c.s)) return e;
+  a.partial = c.kpart();
+  if (int e = launch_conv_any(a, c.s)) return e;
   const BNCoef coef = coef_at(c.sv, L.bn);
   return launch_bn_fwd_finalize(c.part(), gconv_rows(L.fwd), L.fwd.CoutW, L.bn.C, L.bn.Cs,
                                 L.bn.count, c.P + L.bn.gamma, c.P + L.bn.beta,
@@ -520,13 +549,15 @@ int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float 
   if (!dA) return 0;
   tag(L.name, "dgrad");
   if (int e = launch_prep_conv_dgrad(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups,
-                                     L.fold_mod, L.T, L.dgrad.ICs, L.dgrad.CoutW, L.E, c.s))
+                                     L.fold_mod, L.T, L.dgrad.ICs, L.dgrad.CoutW, L.E,
+                                     wpack_of(L.dgrad), c.s))
     return e;
   GConvArgs a = L.dgrad;
   a.in = dy;
   a.w = c.wprep();
   a.out = dA;
-  return launch_gconv(a, c.s);
+  a.partial = c.kpart();
+  return launch_conv_any(a, c.s);
 }
 
 // BatchNorm+ReLU backward for layer L: dbuf holds d(post-activation) on entry
@@ -642,7 +673,23 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
     const ConvTLayer &u = p.up[j];
     tag(u.name, "fwd");
     float *U = c.fptr(c.sv, u.u_off);
-    for (size_t ph = 0; ph < u.phases.size(); ++ph) {
+    if (u.fused) {
+      GConvArgs a = u.fwdf;
+      if (int e = launch_prep_convt_fused(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.K[0], u.K[1],
+                                          u.K[2], u.S[0], u.S[1], u.S[2], a.ICs, a.CoutW,
+                                          wpack_of(a), c.s))
+        return e;
+      a.in = src;
+      a.in_scale = ssc;
+      a.in_shift = ssh;
+      a.w = c.wprep();
+      a.bias = c.P + u.b_off;
+      a.out = U;
+      a.stats = nullptr;
+      a.partial = c.kpart();
+      if (int e = launch_conv_any(a, c.s)) return e;
+    }
+    for (size_t ph = 0; !u.fused && ph < u.phases.size(); ++ph) {
       const int *pj = &u.pJ[ph * 6];
       GConvArgs a = u.phases[ph];
       if (int e = launch_prep_convt_fwd(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.K[0], u.K[1],
@@ -759,14 +806,15 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
     }
     tag(u.name, "dgrad");
     if (int e = launch_prep_convt_dgrad(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.T, u.dgrad.ICs,
-                                        u.dgrad.CoutW, c.s))
+                                        u.dgrad.CoutW, wpack_of(u.dgrad), c.s))
       return e;
     {
       GConvArgs a = u.dgrad;
       a.in = A;
       a.w = c.wprep();
       a.out = Bf;
-      if (int e = launch_gconv(a, c.s)) return e;
+      a.partial = c.kpart();
+      if (int e = launch_conv_any(a, c.s)) return e;
     }
     if (int e = bn_backward(c, prev, Bf, nullptr, nullptr, training, accumulate)) return e;
     cur = 1 - cur;
@@ -804,8 +852,8 @@ namespace {
 struct OpPlan {
   ConvLayer conv;
   ConvTLayer ct;
-  size_t max_wprep = 0, max_part = 0;
-  size_t wprep_off = 0, part_off = 0, scratch_bytes = 0;
+  size_t max_wprep = 0, max_part = 0, max_kpart = 0;
+  size_t wprep_off = 0, part_off = 0, kpart_off = 0, scratch_bytes = 0;
 };
 
 int make_op(const hcu_conv_desc *d, OpPlan &op) {
@@ -818,15 +866,19 @@ int make_op(const hcu_conv_desc *d, OpPlan &op) {
       return e;
     op.max_wprep = std::max(prep_floats_fwd(op.conv), prep_floats_dgrad(op.conv));
     op.max_part = wgrad_partial_floats(op.conv.wg);
+    op.max_kpart = std::max(conv_partial_floats(op.conv.fwd), conv_partial_floats(op.conv.dgrad));
   } else {
     if (d->groups != 1) return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d: groups must be 1");
     for (int i = 0; i < 3; ++i)
       if (d->dil[i] != 1) return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d: dilation must be 1");
-    if (int e = setup_convt(op.ct, in, d->Cout, d->k, d->stride, op.max_wprep, op.max_part)) return e;
+    if (int e = setup_convt(op.ct, in, d->Cout, d->k, d->stride, op.max_wprep, op.max_part,
+                            op.max_kpart))
+      return e;
   }
   Region r;
   op.wprep_off = r.take_floats(op.max_wprep);
   op.part_off = r.take_floats(op.max_part);
+  op.kpart_off = r.take_floats(std::max<size_t>(op.max_kpart, 1));
   op.scratch_bytes = r.off;
   return 0;
 }
@@ -864,19 +916,33 @@ int hcu_conv_fwd_cl(const hcu_conv_desc *d, const float *x, const float *w, cons
   if (int e = check_scratch(op, scratch, scratch_bytes)) return e;
   hipStream_t s = (hipStream_t)stream;
   float *wprep = reinterpret_cast<float *>((char *)scratch + op.wprep_off);
+  float *kpart = reinterpret_cast<float *>((char *)scratch + op.kpart_off);
   if (!d->transposed) {
     const ConvLayer &L = op.conv;
     if (int e = launch_prep_conv_fwd(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
-                                     L.fwd.ICs, L.fwd.CoutW, s))
+                                     L.fwd.ICs, L.fwd.CoutW, wpack_of(L.fwd), s))
       return e;
     GConvArgs a = L.fwd;
     a.in = x;
     a.w = wprep;
     a.bias = bias;
     a.out = y;
-    return launch_gconv(a, s);
+    a.partial = kpart;
+    return launch_conv_any(a, s);
   }
   const ConvTLayer &u = op.ct;
+  if (u.fused) {
+    GConvArgs a = u.fwdf;
+    if (int e = launch_prep_convt_fused(w, wprep, u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0],
+                                        u.S[1], u.S[2], a.ICs, a.CoutW, wpack_of(a), s))
+      return e;
+    a.in = x;
+    a.w = wprep;
+    a.bias = bias;
+    a.out = y;
+    a.partial = kpart;
+    return launch_conv_any(a, s);
+  }
   for (size_t ph = 0; ph < u.phases.size(); ++ph) {
     const int *pj = &u.pJ[ph * 6];
     GConvArgs a = u.phases[ph];
@@ -900,23 +966,26 @@ int hcu_conv_dgrad_cl(const hcu_conv_desc *d, const float *dy, const float *w, f
   if (int e = check_scratch(op, scratch, scratch_bytes)) return e;
   hipStream_t s = (hipStream_t)stream;
   float *wprep = reinterpret_cast<float *>((char *)scratch + op.wprep_off);
+  float *kpart = reinterpret_cast<float *>((char *)scratch + op.kpart_off);
   GConvArgs a;
   if (!d->transposed) {
     const ConvLayer &L = op.conv;
     if (int e = launch_prep_conv_dgrad(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
-                                       L.dgrad.ICs, L.dgrad.CoutW, L.E, s))
+                                       L.dgrad.ICs, L.dgrad.CoutW, L.E, wpack_of(L.dgrad), s))
       return e;
     a = L.dgrad;
   } else {
     const ConvTLayer &u = op.ct;
-    if (int e = launch_prep_convt_dgrad(w, wprep, u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW, s))
+    if (int e = launch_prep_convt_dgrad(w, wprep, u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW,
+                                        wpack_of(u.dgrad), s))
       return e;
     a = u.dgrad;
   }
   a.in = dy;
   a.w = wprep;
   a.out = dx;
-  return launch_gconv(a, s);
+  a.partial = kpart;
+  return launch_conv_any(a, s);
 }
 
 int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy, float *dw,
