@@ -144,6 +144,9 @@ struct WGradArgs {
   int mchunks, nchunks, KB;
   int lds_bytes;
   FastDiv fHAZ, fHAY, fHGZ, fHGY, fTZ, fTY;
+  // wgrad2 (Conv3d, stride-1 operands): z rows padded to multiples of 4 so a
+  // lane reads 4 consecutive voxels with one ds_read_b128; one A image per kz.
+  int v2, TZP, HAZP, PA2, PG2, gridx, occ;
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 int plan_wgrad(WGradArgs &a, int target_blocks);

@@ -52,6 +52,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   float *wlds = smem + ((HV * CKP + 3) & ~3);          // [S][4][NT][4]
   int *toffs = reinterpret_cast<int *>(wlds + S * 4 * NT * 4);  // [S][4]
   int *rowpk = toffs + S * 4;                                    // [MPW*64] (lx,ly,lz) of GEMM rows
+  int *rowoff = rowpk + MPW * 64;                                // [MPW*64] store offset in the tile
 
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
@@ -82,6 +83,9 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
       a.fTZ.divmod(i, q, lz);
       a.fTY.divmod(q, lx, ly);
       pk = (lx << 20) | (ly << 10) | lz;
+      rowoff[i] = ((lx * a.osx * a.SY + ly * a.osy) * a.SZ + lz * a.osz) * a.OCs;
+    } else {
+      rowoff[i] = -1;
     }
     rowpk[i] = pk;
   }
@@ -147,22 +151,41 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   floatx4 acc[MPW][NSUB];
   // Subtiles past the tile (m >= nmsub) read voxel 0 and are never stored, so
   // the step body has no per-subtile branch and the MFMA chains interleave.
+  // Software-pipelined over the K-steps with two register sets: the fragments
+  // of step s+1 are loaded before the MFMAs of step s (a scheduling barrier
+  // keeps that order), so the LDS latency hides behind 4*MPW*NSUB MFMAs.
+  auto load_frag = [&](int s, int toff, floatx4 (&bfr)[NSUB], floatx4 (&afr)[MPW]) {
+    const int ss = min(s, S - 1);  // past the end: re-read valid LDS, never used
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n)
+      bfr[n] = *reinterpret_cast<const floatx4 *>(wlds + ((ss * 4 + g) * NT + n * 16 + r16) * 4);
+#pragma unroll
+    for (int j = 0; j < MPW; ++j) afr[j] = *reinterpret_cast<const floatx4 *>(alds + vb[j] + toff);
+  };
+  auto toff_of = [&](int s) { return toffs[min(s, S - 1) * 4 + g]; };
+  auto mfma_frag = [&](const floatx4 (&bfr)[NSUB], const floatx4 (&afr)[MPW]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int j = 0; j < MPW; ++j)
+#pragma unroll
+        for (int n = 0; n < NSUB; ++n)
+          acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(afr[j][c], bfr[n][c], acc[j][n], 0, 0, 0);
+  };
   auto compute = [&]() {
-    for (int s = 0; s < S; ++s) {
-      const int toff = toffs[s * 4 + g];
-      floatx4 bf[NSUB], av[MPW];
-#pragma unroll
-      for (int n = 0; n < NSUB; ++n)
-        bf[n] = *reinterpret_cast<const floatx4 *>(wlds + ((s * 4 + g) * NT + n * 16 + r16) * 4);
-#pragma unroll
-      for (int j = 0; j < MPW; ++j) av[j] = *reinterpret_cast<const floatx4 *>(alds + vb[j] + toff);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int j = 0; j < MPW; ++j)
-#pragma unroll
-          for (int n = 0; n < NSUB; ++n)
-            acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j][c], bf[n][c], acc[j][n], 0, 0, 0);
+    floatx4 b0[NSUB], a0[MPW], b1[NSUB], a1[MPW];
+    int tA = toff_of(0), tB = toff_of(1);
+    load_frag(0, tA, b0, a0);
+    tA = toff_of(2);
+    for (int s = 0; s < S; s += 2) {
+      load_frag(s + 1, tB, b1, a1);
+      tB = toff_of(s + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_frag(b0, a0);
+      load_frag(s + 2, tA, b0, a0);
+      tA = toff_of(s + 4);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < S) mfma_frag(b1, a1);
     }
   };
 
@@ -193,35 +216,41 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   }
   const bool zpad = a.nph > 1 && a.OCs > a.Cout;
   auto epilogue = [&](int b, int ox0, int oy0, int oz0) {
+    float *tp = dst + ((((size_t)b * a.SX + ox0 * a.osx + a.ofx) * a.SY + oy0 * a.osy + a.ofy) *
+                           a.SZ + oz0 * a.osz + a.ofz) * a.OCs;
+    const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
 #pragma unroll
     for (int j = 0; j < MPW; ++j) {
       const int m = wave + 4 * j;
       if (m < nmsub) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int pk = rowpk[m * 16 + g * 4 + r];
-          if (pk >= 0) {
-            const int ox = ox0 + (pk >> 20), oy = oy0 + ((pk >> 10) & 1023), oz = oz0 + (pk & 1023);
-            if (ox < a.OX && oy < a.OY && oz < a.OZ) {
-              const size_t vbase = ((((size_t)b * a.SX + ox * a.osx + a.ofx) * a.SY +
-                                     oy * a.osy + a.ofy) * a.SZ + oz * a.osz + a.ofz) * a.OCs;
+          const int i = m * 16 + g * 4 + r;
+          const int ro = rowoff[i];
+          bool ok = ro >= 0;
+          if (ok && !interior) {
+            const int pk = rowpk[i];
+            ok = ox0 + (pk >> 20) < a.OX && oy0 + ((pk >> 10) & 1023) < a.OY &&
+                 oz0 + (pk & 1023) < a.OZ;
+          }
+          if (ok) {
+            float *vp = tp + ro;
+#pragma unroll
+            for (int n = 0; n < NSUB; ++n) {
+              if (coff[n] < 0) continue;
+              const float val = acc[j][n][r] + bias_v[n];
+              vp[coff[n]] = val;
+              if (cst[n]) {
+                s1[n] += val;
+                s2[n] = fmaf(val, val, s2[n]);
+              }
+            }
+            if (zpad) {   // ConvTranspose3d phases: zero the padded channels of U
 #pragma unroll
               for (int n = 0; n < NSUB; ++n) {
-                if (coff[n] < 0) continue;
-                const float val = acc[j][n][r] + bias_v[n];
-                dst[vbase + coff[n]] = val;
-                if (cst[n]) {
-                  s1[n] += val;
-                  s2[n] = fmaf(val, val, s2[n]);
-                }
-              }
-              if (zpad) {   // ConvTranspose3d phases: zero the padded channels of U
-#pragma unroll
-                for (int n = 0; n < NSUB; ++n) {
-                  const int nn = n0 + n * 16 + r16;
-                  if (coff[n] >= 0 && nn % a.Cout == a.Cout - 1)
-                    for (int cz = 1; cz <= a.OCs - a.Cout; ++cz) dst[vbase + coff[n] + cz] = 0.f;
-                }
+                const int nn = n0 + n * 16 + r16;
+                if (coff[n] >= 0 && nn % a.Cout == a.Cout - 1)
+                  for (int cz = 1; cz <= a.OCs - a.Cout; ++cz) vp[coff[n] + cz] = 0.f;
               }
             }
           }
@@ -454,7 +483,7 @@ static long conv2_lds(const GConvArgs &a, int CK, int NT) {
   const int TPS = 16 / CK;
   const int S = (T + TPS - 1) / TPS;
   const long HV = (long)a.HX * a.HY * a.HZ;
-  return (((HV * (CK + 4) + 3) & ~3L) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 64) * 4;
+  return (((HV * (CK + 4) + 3) & ~3L) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128) * 4;
 }
 
 // Chooses CK / NSUB / MPW / tile / K split / prefetch depth / grid for

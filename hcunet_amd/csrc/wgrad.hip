@@ -13,8 +13,17 @@
 #include "common.h"
 #include "timing.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace hcu {
+
+bool wgrad2_disabled() {   // HCU_NO_WGRAD2=1 forces the generic kernel (A/B testing)
+  static const bool off = [] {
+    const char *e = getenv("HCU_NO_WGRAD2");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
 
 template <int NS, int MSMAX>
 __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
@@ -225,6 +234,299 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// wgrad2: Conv3d weight gradient with b128 operand reads.
+//   dW[(t,ci)][co] = sum_p act(A[p + off(t)][ci]) * G[p][co]   (+ bias row: sum_p G[p][co])
+// K = voxels p of a TX*TY*TZP tile (TZP = TZ rounded up to 4, the extra z
+// positions have G = 0).  A K-step is 16 voxels: lane group g takes the 4
+// z-consecutive voxels 4g..4g+3 with ONE ds_read_b128 from a channel-major LDS
+// image, component j feeding MFMA j (a permutation of the voxel sum).  To keep
+// every b128 16-byte aligned the A halo is staged once per kz tap shift
+// (image kz holds A[.., z + kz*dz]); rows of invalid (tap, channel) pairs read
+// a zero image and the bias row reads an image of ones.
+// Workgroups are persistent over tiles and each writes ONE fp32 partial slab;
+// wgrad_finalize sums the slabs in a fixed order.
+template <int NS, int MS>
+__global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int T = a.KX * a.KY * a.KZ;
+  const int CKA = a.CKA, CKG = a.CKG;
+  const int tapc = blockIdx.y / a.nci, cic = blockIdx.y % a.nci, coc = blockIdx.z;
+  const int ci0 = cic * CKA, co0 = coc * CKG;
+  const int t0 = tapc * a.TA;
+  const bool bias_block = a.bias_row && tapc == 0 && cic == 0;
+  const int PA = a.PA2, PG = a.PG2;
+  const int HAZP = a.HAZP, HAYZP = a.HAY * a.HAZP;
+  const int nimg = a.KZ * CKA;                 // A images: [kz][c]
+  float *alds = smem;                          // [nimg + 2][PA]  (+ zero, ones)
+  float *glds = alds + (size_t)(nimg + 2) * PA;  // [CKG + 1][PG]   (+ zero)
+  int *hvtab = reinterpret_cast<int *>(glds + (size_t)(CKG + 1) * PG);
+  const int TZP = a.TZP;
+  const int PT4 = a.TX * a.TY * TZP / 4;       // voxel quads of a tile
+  const int nks = (PT4 + 3) / 4;               // 16-voxel K-steps (tail quads: G = 0)
+
+  // zero everything once: padded z positions and unused rows stay finite (0)
+  for (int i = tid; i < (nimg + 2) * PA + (CKG + 1) * PG; i += 256) smem[i] = 0.f;
+  __syncthreads();
+  for (int i = tid; i < PA; i += 256) alds[(size_t)(nimg + 1) * PA + i] = 1.f;
+  for (int q = tid; q < nks * 4; q += 256) {
+    const int p = q * 4;
+    const int lz = p % TZP, r = p / TZP, ly = r % a.TY, lx = r / a.TY;
+    hvtab[q] = q < PT4 ? lx * HAYZP + ly * HAZP + lz : 0;
+  }
+  // per-lane row images (A side) and column images (G side)
+  int aoff[MS];
+#pragma unroll
+  for (int ms = 0; ms < MS; ++ms) {
+    const int lr = ms * 16 + r16;
+    int off = nimg * PA;  // zero image
+    const int tl = lr / CKA, c = lr % CKA, ta = t0 + tl;
+    if (tl < a.TA) {
+      if (ta < T && ci0 + c < a.ACs) {
+        const int kz = ta % a.KZ, q = ta / a.KZ, ky = q % a.KY, kx = q / a.KY;
+        off = (kz * CKA + c) * PA + kx * a.adx * HAYZP + ky * a.ady * HAZP;
+      }
+    } else if (bias_block && lr == a.TA * CKA) {
+      off = (nimg + 1) * PA;  // ones image
+    }
+    aoff[ms] = off;
+  }
+  int goff[NS];
+#pragma unroll
+  for (int ns = 0; ns < NS; ++ns) {
+    const int lc = ns * 16 + r16;
+    goff[ns] = (lc < CKG && co0 + lc < a.GCs) ? lc * PG : CKG * PG;
+  }
+
+  floatx4 acc[MS][NS];
+#pragma unroll
+  for (int ms = 0; ms < MS; ++ms)
+#pragma unroll
+    for (int ns = 0; ns < NS; ++ns) acc[ms][ns] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int CA4 = CKA / 4, CG4 = CKG / 4;
+  const int HAV = a.HAX * a.HAY * a.HAZ;        // real halo extent
+  const int PTr = a.TX * a.TY * a.TZ;           // real tile extent
+
+  for (int tt = blockIdx.x; tt < total; tt += gridDim.x) {
+    const int b = tt / ntiles;
+    int tile = tt - b * ntiles;
+    const int tzi = tile % a.ntz;
+    tile /= a.ntz;
+    const int tyi = tile % a.nty, txi = tile / a.nty;
+    const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    __syncthreads();
+    // ---- A halo -> one channel-major image per kz shift (act applied, 0 outside)
+    for (int base = tid; base < HAV * CA4; base += 4 * 256) {
+      float4 val[4];
+      int vv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = base + u * 256;
+        val[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        vv[u] = -1;
+        if (idx < HAV * CA4) {
+          const int c4 = idx % CA4, v = idx / CA4;
+          int q, hz, hx, hy;
+          a.fHAZ.divmod(v, q, hz);
+          a.fHAY.divmod(q, hx, hy);
+          vv[u] = (((hx << 10) | hy) << 10 | hz) * 8 + c4;  // c4 < 8
+          const int gx = px0 + hx, gy = py0 + hy, gz = pz0 + hz;
+          const int c = ci0 + c4 * 4;
+          if (gx < a.AX && gy < a.AY && gz < a.AZ && c < a.ACs) {
+            val[u] = *reinterpret_cast<const float4 *>(
+                a.A + ((((size_t)b * a.AX + gx) * a.AY + gy) * a.AZ + gz) * a.ACs + c);
+            if (a.a_scale) {
+              const float4 sc = *reinterpret_cast<const float4 *>(a.a_scale + c);
+              const float4 sh = *reinterpret_cast<const float4 *>(a.a_shift + c);
+              val[u].x = fmaxf(fmaf(val[u].x, sc.x, sh.x), 0.f);
+              val[u].y = fmaxf(fmaf(val[u].y, sc.y, sh.y), 0.f);
+              val[u].z = fmaxf(fmaf(val[u].z, sc.z, sh.z), 0.f);
+              val[u].w = fmaxf(fmaf(val[u].w, sc.w, sh.w), 0.f);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (vv[u] < 0) continue;
+        const int c4 = vv[u] & 7, pk = vv[u] >> 3;
+        const int hz = pk & 1023, hy = (pk >> 10) & 1023, hx = pk >> 20;
+        for (int kz = 0; kz < a.KZ; ++kz) {
+          const int z = hz - kz * a.adz;
+          if (z < 0 || z >= HAZP) continue;
+          float *d = alds + (size_t)(kz * CKA + c4 * 4) * PA + hx * HAYZP + hy * HAZP + z;
+          d[0] = val[u].x;
+          d[PA] = val[u].y;
+          d[2 * PA] = val[u].z;
+          d[3 * PA] = val[u].w;
+        }
+      }
+    }
+    // ---- G tile -> channel-major [co][p] with z rows of TZP (0 outside)
+    for (int base = tid; base < PTr * CG4; base += 4 * 256) {
+      float4 val[4];
+      int pp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int idx = base + u * 256;
+        val[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pp[u] = -1;
+        if (idx < PTr * CG4) {
+          const int c4 = idx % CG4, p = idx / CG4;
+          int q, lz, lx, ly;
+          a.fTZ.divmod(p, q, lz);
+          a.fTY.divmod(q, lx, ly);
+          pp[u] = ((lx * a.TY + ly) * TZP + lz) * 32 + c4;  // c4 < 32
+          const int gx = px0 + lx, gy = py0 + ly, gz = pz0 + lz;
+          const int c = co0 + c4 * 4;
+          if (gx < a.PX && gy < a.PY && gz < a.PZ && c < a.GCs)
+            val[u] = *reinterpret_cast<const float4 *>(
+                a.G + ((((size_t)b * a.GX + gx) * a.GY + gy) * a.GZ + gz) * a.GCs + c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (pp[u] < 0) continue;
+        const int c4 = pp[u] & 31, p = pp[u] >> 5;
+        float *d = glds + (size_t)(c4 * 4) * PG + p;
+        d[0] = val[u].x;
+        d[PG] = val[u].y;
+        d[2 * PG] = val[u].z;
+        d[3 * PG] = val[u].w;
+      }
+    }
+    __syncthreads();
+    // ---- MFMA over the tile's voxels: wave w takes K-steps w, w+4, ...
+    for (int ks = wave; ks < nks; ks += 4) {
+      const int q = ks * 4 + g;
+      const int hv = hvtab[q];
+      floatx4 bv[NS], av[MS];
+#pragma unroll
+      for (int ns = 0; ns < NS; ++ns)
+        bv[ns] = *reinterpret_cast<const floatx4 *>(glds + goff[ns] + q * 4);
+#pragma unroll
+      for (int ms = 0; ms < MS; ++ms)
+        av[ms] = *reinterpret_cast<const floatx4 *>(alds + aoff[ms] + hv);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int ms = 0; ms < MS; ++ms)
+#pragma unroll
+            for (int ns = 0; ns < NS; ++ns)
+              acc[ms][ns] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ms][c], bv[ns][c], acc[ms][ns], 0, 0, 0);
+    }
+  }
+
+  // ---- cross-wave reduction in a fixed order, then one partial slab write
+  __syncthreads();
+  float *red = smem;  // [MS*NS][64][4]
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int ms = 0; ms < MS; ++ms) {
+        {
+#pragma unroll
+          for (int ns = 0; ns < NS; ++ns) {
+            float *dst = red + ((ms * NS + ns) * 64 + lane) * 4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[r] = (w == 0) ? acc[ms][ns][r] : dst[r] + acc[ms][ns][r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int kb = blockIdx.x;
+  const int nel = MS * NS * 256;
+  for (int idx = tid; idx < nel; idx += 256) {
+    const int r = idx & 3, ln = (idx >> 2) & 63, ti = idx >> 8;
+    const int ms = ti / NS, ns = ti % NS;
+    const int lr = ms * 16 + (ln >> 4) * 4 + r;
+    const int lc = ns * 16 + (ln & 15);
+    int grow = -1, gcol = -1;
+    const int tl = lr / CKA, ta = t0 + tl;
+    if (tl < a.TA) {
+      const int ci = ci0 + lr % CKA;
+      if (ta < T && ci < a.ACs) grow = ta * a.ACs + ci;
+    } else if (bias_block && lr == a.TA * CKA) {
+      grow = T * a.ACs;
+    }
+    if (lc < CKG && co0 + lc < a.GCs) gcol = co0 + lc;
+    if (grow >= 0 && gcol >= 0)
+      a.partial[((size_t)kb * a.Mtot + grow) * a.Ntot + gcol] = red[idx];
+  }
+}
+
+// Re-plans a Conv3d wgrad (taps_rows, stride-1 operands) for wgrad2_kernel:
+// tile, padded LDS images, persistent grid.  Returns 0 when wgrad2 applies.
+static int plan_wgrad2(WGradArgs &a, int target_blocks) {
+  a.v2 = 0;
+  if (!a.taps_rows || a.asx != 1 || a.asy != 1 || a.asz != 1 || a.gsx != 1 || a.gsy != 1 ||
+      a.gsz != 1 || a.apx || a.apy || a.apz || a.gpx || a.gpy || a.gpz)
+    return 1;
+  if (a.CKA % 4 || a.CKA > 32 || a.CKG > 128) return 1;
+  const int ntz = cdiv(a.PZ, 16);
+  const int TZ = cdiv(a.PZ, ntz);
+  const int TZP = round_up(TZ, 4);
+  const int HAZ = TZ + (a.KZ - 1) * a.adz;
+  const int HAZP = TZP;  // image z rows: the voxels p read z in [0, TZP)
+  (void)HAZ;
+  const int nimg = a.KZ * a.CKA;
+  const int txys[5][2] = {{8, 8}, {6, 8}, {4, 8}, {4, 4}, {2, 4}};
+  int best = -1;
+  long lds = 0;
+  for (int i = 0; i < 5; ++i) {
+    const int TX = std::min(txys[i][0], a.PX), TY = std::min(txys[i][1], a.PY);
+    const int HAX = TX + (a.KX - 1) * a.adx, HAY = TY + (a.KY - 1) * a.ady;
+    int PA = HAX * HAY * HAZP;
+    PA = round_up(PA, 64) + 4;
+    const int nq = round_up(TX * TY * TZP / 4, 4);   // quads incl. the zero tail
+    int PG = nq * 4;
+    PG = round_up(PG, 64) + 4;
+    const long bytes = ((long)(nimg + 2) * PA + (long)(a.CKG + 1) * PG + nq) * 4;
+    const long red = (long)a.MS * a.NS * 256 * 4;
+    const long need = std::max(bytes, red);
+    if (need <= 48 * 1024 || i == 4) {
+      best = i;
+      lds = need;
+      a.TX = TX;
+      a.TY = TY;
+      a.HAX = HAX;
+      a.HAY = HAY;
+      a.PA2 = PA;
+      a.PG2 = PG;
+      break;
+    }
+  }
+  if (best < 0 || lds > 64 * 1024) return 1;
+  a.TZ = TZ;
+  a.TZP = TZP;
+  a.HAZ = HAZ;
+  a.HAZP = HAZP;
+  a.lds_bytes = (int)lds;
+  a.fHAZ = FastDiv(a.HAZ);
+  a.fHAY = FastDiv(a.HAY);
+  a.fTZ = FastDiv(a.TZ);
+  a.fTY = FastDiv(a.TY);
+  a.ntx = cdiv(a.PX, a.TX);
+  a.nty = cdiv(a.PY, a.TY);
+  a.ntz = ntz;
+  const long total = (long)a.B * a.ntx * a.nty * a.ntz;
+  const long per = (long)a.mchunks * a.nchunks;
+  a.occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
+  long kb = std::max(1L, (long)256 * a.occ / per);
+  kb = std::min(kb, total);
+  a.KB = (int)kb;
+  a.v2 = 1;
+  (void)target_blocks;
+  return 0;
+}
+
 int plan_wgrad(WGradArgs &a, int target_blocks) {
   const int T = a.KX * a.KY * a.KZ;
   if (a.ACs % 4 || a.GCs % 4) return fail(1, "wgrad: channel strides must be multiples of 4");
@@ -321,12 +623,34 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   long kb = std::max(1L, (long)target_blocks / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
+  if (!wgrad2_disabled()) plan_wgrad2(a, target_blocks);
   return 0;
 }
 
 int launch_wgrad(const WGradArgs &a, hipStream_t s) {
   const dim3 grid(a.KB, a.mchunks, a.nchunks);
   const int T = a.KX * a.KY * a.KZ;
+  if (a.v2) {
+    const double fl2 = a.flops > 0 ? a.flops
+                                   : 2.0 * a.B * a.PX * a.PY * a.PZ * (double)T * a.ACs * a.GCs;
+    const double by2 = 4.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
+                              (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
+    bool ok = false;
+#define W2(NS_, MS_)                                                                       \
+  if (!ok && a.NS == NS_ && a.MS == MS_) {                                                 \
+    HCU_TIMED(s, "wgrad2_kernel<" #NS_ "," #MS_ ">", fl2, by2,                              \
+              hipLaunchKernelGGL((wgrad2_kernel<NS_, MS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    ok = true;                                                                             \
+  }
+    W2(1, 1) W2(1, 2) W2(1, 3) W2(1, 4) W2(1, 5) W2(1, 6) W2(1, 7) W2(1, 8)
+    W2(1, 9) W2(1, 10) W2(1, 11) W2(1, 12) W2(1, 13) W2(1, 14) W2(1, 15) W2(1, 16)
+    W2(2, 1) W2(2, 2) W2(2, 3) W2(2, 4) W2(2, 5) W2(2, 6) W2(2, 7) W2(2, 8)
+    W2(4, 1) W2(4, 2) W2(4, 3) W2(4, 4)
+#undef W2
+    if (!ok) return fail(4, "wgrad2: unsupported variant");
+    HCU_CHECK_LAUNCH();
+    return 0;
+  }
   const double fl = a.flops > 0 ? a.flops
                                 : 2.0 * a.B * a.PX * a.PY * a.PZ * (double)T * a.ACs * a.GCs;
   const double by = 4.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
