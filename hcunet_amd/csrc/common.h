@@ -85,6 +85,9 @@ struct GConvArgs {
   float *partial;                     // [ksplit][stored tensor] when ksplit > 1
   int use_conv2;
   int NPF, gridx;                     // conv2 halo prefetch depth, persistent grid size
+  int epi_lds, nc4, areg;             // conv2 epilogue through LDS (float4 stores), float4
+                                      // groups, floats of the halo / C-tile LDS region
+  FastDiv fNT, fNTZ, fNTY;            // tile index decomposition
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 // Chooses the tile and kernel variant; returns 0 or an error code.

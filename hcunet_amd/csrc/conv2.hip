@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   const int HV = a.HX * HYZ;
   const int nel = HV * C4;             // float4 elements of one halo image
   float *alds = smem;                                  // [HV][CKP]
-  float *wlds = smem + ((HV * CKP + 3) & ~3);          // [S][4][NT][4]
+  float *wlds = smem + a.areg;                         // [S][4][NT][4] (areg >= HV*CKP, C tile)
   int *toffs = reinterpret_cast<int *>(wlds + S * 4 * NT * 4);  // [S][4]
   int *rowpk = toffs + S * 4;                                    // [MPW*64] (lx,ly,lz) of GEMM rows
   int *rowoff = rowpk + MPW * 64;                                // [MPW*64] store offset in the tile
@@ -101,12 +101,10 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   }
 
   auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
-    b = tile / ntiles;
-    int r = tile - b * ntiles;
-    const int tzi = r % a.ntz;
-    r /= a.ntz;
-    const int tyi = r % a.nty;
-    const int txi = r / a.nty;
+    int r, tzi, tyi, txi;
+    a.fNT.divmod(tile, b, r);
+    a.fNTZ.divmod(r, r, tzi);
+    a.fNTY.divmod(r, txi, tyi);
     ox0 = txi * a.TX;
     oy0 = tyi * a.TY;
     oz0 = tzi * a.TZ;
@@ -259,6 +257,66 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     }
   };
 
+  // Epilogue through LDS: the accumulator tile is written to LDS (reusing the
+  // halo image) and stored back as float4 runs of 4 channels with bias, so
+  // every store instruction writes whole 16-byte channel groups.  Thread tid
+  // always owns channel group c4 = tid % nc4 (256 % nc4 == 0).
+  const int NTP = NT + 4;
+  const int nc4 = a.nc4;
+  const int ec4 = tid % max(nc4, 1);
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (a.epi_lds && !split && a.bias) {
+    const int cc = n0 + ec4 * 4;
+    bias4.x = cc + 0 < a.Cout ? a.bias[cc + 0] : 0.f;
+    bias4.y = cc + 1 < a.Cout ? a.bias[cc + 1] : 0.f;
+    bias4.z = cc + 2 < a.Cout ? a.bias[cc + 2] : 0.f;
+    bias4.w = cc + 3 < a.Cout ? a.bias[cc + 3] : 0.f;
+  }
+  float4 st1 = make_float4(0.f, 0.f, 0.f, 0.f), st2 = st1;
+  auto epilogue_lds = [&](int b, int ox0, int oy0, int oz0) {
+    __syncthreads();  // every wave is done reading the halo image
+#pragma unroll
+    for (int j = 0; j < MPW; ++j) {
+      const int m = wave + 4 * j;
+      if (m < nmsub) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int n = 0; n < NSUB; ++n)
+            smem[(m * 16 + g * 4 + r) * NTP + n * 16 + r16] = acc[j][n][r];
+      }
+    }
+    __syncthreads();
+    float *tp = dst + ((((size_t)b * a.SX + ox0 * a.osx + a.ofx) * a.SY + oy0 * a.osy + a.ofy) *
+                           a.SZ + oz0 * a.osz + a.ofz) * a.OCs + n0 + ec4 * 4;
+    const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
+    const int vstep = 256 / nc4;
+    for (int i = tid / nc4; i < MT; i += vstep) {
+      bool ok = true;
+      if (!interior) {
+        const int pk = rowpk[i];
+        ok = ox0 + (pk >> 20) < a.OX && oy0 + ((pk >> 10) & 1023) < a.OY && oz0 + (pk & 1023) < a.OZ;
+      }
+      if (ok) {
+        float4 v = *reinterpret_cast<const float4 *>(smem + i * NTP + ec4 * 4);
+        v.x += bias4.x;
+        v.y += bias4.y;
+        v.z += bias4.z;
+        v.w += bias4.w;
+        *reinterpret_cast<float4 *>(tp + rowoff[i]) = v;
+        st1.x += v.x; st1.y += v.y; st1.z += v.z; st1.w += v.w;
+        st2.x = fmaf(v.x, v.x, st2.x);
+        st2.y = fmaf(v.y, v.y, st2.y);
+        st2.z = fmaf(v.z, v.z, st2.z);
+        st2.w = fmaf(v.w, v.w, st2.w);
+      }
+    }
+  };
+  auto finish_tile = [&](int b, int ox0, int oy0, int oz0) {
+    if (a.epi_lds) epilogue_lds(b, ox0, oy0, oz0);
+    else epilogue(b, ox0, oy0, oz0);
+  };
+
   if (NPF > 0 && ce - cb == 1) {
     // ---- single channel chunk: weights staged once, next tile's halo in flight.
     // Thread tid always handles channel group c4 = tid % C4 of halo voxels
@@ -294,14 +352,16 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
       tile_origin(tile, b, x0, y0, z0);
       const int gx0 = x0 * a.sx - a.px, gy0 = y0 * a.sy - a.py, gz0 = z0 * a.sz - a.pz;
       const int64_t base = ((((int64_t)b * a.IX + gx0) * a.IY + gy0) * a.IZ + gz0) * a.ICs + c;
+      const bool inb = gx0 >= 0 && gy0 >= 0 && gz0 >= 0 && gx0 + a.HX <= a.IX &&
+                       gy0 + a.HY <= a.IY && gz0 + a.HZ <= a.IZ;
 #pragma unroll
       for (int u = 0; u < NPF; ++u) {
         float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
         const int hp = hpk[u];
         if (hp >= 0) {
           const int gx = gx0 + (hp >> 20), gy = gy0 + ((hp >> 10) & 1023), gz = gz0 + (hp & 1023);
-          if ((unsigned)gx < (unsigned)a.IX && (unsigned)gy < (unsigned)a.IY &&
-              (unsigned)gz < (unsigned)a.IZ) {
+          if (inb || ((unsigned)gx < (unsigned)a.IX && (unsigned)gy < (unsigned)a.IY &&
+                      (unsigned)gz < (unsigned)a.IZ)) {
             val = *reinterpret_cast<const float4 *>(a.in + base + goff[u]);
             if (act) {
               val.x = fmaxf(fmaf(val.x, sc.x, sh.x), 0.f);
@@ -330,7 +390,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       compute();
-      epilogue(b, ox0, oy0, oz0);
+      finish_tile(b, ox0, oy0, oz0);
     }
   } else {
     for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
@@ -361,11 +421,29 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
         __syncthreads();
         compute();
       }
-      epilogue(b, ox0, oy0, oz0);
+      finish_tile(b, ox0, oy0, oz0);
     }
   }
 
-  if (a.stats && !split) {
+  if (a.stats && !split && a.epi_lds) {
+    // fixed-order combine of the threads that share a channel group
+    __syncthreads();
+    float *red = smem;  // [256][8]
+    red[tid * 8 + 0] = st1.x; red[tid * 8 + 1] = st1.y; red[tid * 8 + 2] = st1.z; red[tid * 8 + 3] = st1.w;
+    red[tid * 8 + 4] = st2.x; red[tid * 8 + 5] = st2.y; red[tid * 8 + 6] = st2.z; red[tid * 8 + 7] = st2.w;
+    __syncthreads();
+    if (tid < nc4 * 4) {
+      const int c4 = tid >> 2, comp = tid & 3;
+      float t1 = 0.f, t2 = 0.f;
+      for (int k = c4; k < 256; k += nc4) {
+        t1 += red[k * 8 + comp];
+        t2 += red[k * 8 + 4 + comp];
+      }
+      const size_t row = blockIdx.x;
+      a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
+      a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+    }
+  } else if (a.stats && !split) {
 #pragma unroll
     for (int n = 0; n < NSUB; ++n) {
       s1[n] += __shfl_xor(s1[n], 16);
@@ -478,12 +556,18 @@ static void tile2(int OX, int OY, int TZ, int maxM, int &TX, int &TY) {
   if (TY > OY) { TY = OY; TX = std::max(1, std::min(OX, txy / TY)); }
 }
 
+static long conv2_areg(const GConvArgs &a, int CK, int NT) {
+  const long HV = (long)a.HX * a.HY * a.HZ;
+  const long ctile = (long)a.MPW * 64 * (NT + 4);   // LDS epilogue tile
+  return (std::max(HV * (CK + 4), ctile) + 3) & ~3L;
+}
+
 static long conv2_lds(const GConvArgs &a, int CK, int NT) {
   const int T = a.KX * a.KY * a.KZ;
   const int TPS = 16 / CK;
   const int S = (T + TPS - 1) / TPS;
-  const long HV = (long)a.HX * a.HY * a.HZ;
-  return (((HV * (CK + 4) + 3) & ~3L) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128) * 4;
+  return std::max(conv2_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128,
+                  256L * 8) * 4;
 }
 
 // Chooses CK / NSUB / MPW / tile / K split / prefetch depth / grid for
@@ -562,6 +646,15 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
   a.fHY = FastDiv(a.HY);
   a.fTZ = FastDiv(a.TZ);
   a.fTY = FastDiv(a.TY);
+  a.fNT = FastDiv(a.ntx * a.nty * a.ntz);
+  a.fNTZ = FastDiv(a.ntz);
+  a.fNTY = FastDiv(a.nty);
+  // LDS epilogue: plain layouts whose float4 channel groups divide 256
+  a.nc4 = std::min(NT, a.OCs) / 4;
+  a.epi_lds = 0;
+  if (a.nph == 1 && (a.CoutW / NT == 1 || a.OCs % NT == 0) && a.nc4 > 0 && 256 % a.nc4 == 0)
+    a.epi_lds = 1;
+  a.areg = (int)conv2_areg(a, a.CK, NT);
   a.use_conv2 = 1;
   return 0;
 }
