@@ -298,6 +298,25 @@ int launch_prep_convt_fused(const float *w, float *wg, int Cin, int Cout, int KX
 int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T,
                             int UCs, int CinW, WPack pk, hipStream_t s);
 
+// Batched weight preparation: every re-layout of one network step in a few
+// launches (one workgroup row per job) instead of one launch per layer.
+enum PrepKind { PREP_CONV_FWD = 0, PREP_CONV_DGRAD = 1, PREP_CONVT_FUSED = 2,
+                PREP_CONVT_PHASE = 3, PREP_CONVT_DGRAD = 4 };
+struct PrepJob {
+  int kind, pad;
+  int64_t n;        // elements of the prepared buffer
+  int64_t src;      // float offset of the PyTorch-layout weight in the parameter buffer
+  int64_t dst;      // float offset of the prepared buffer in the destination workspace
+  WPack pk;
+  // CONV_FWD / CONV_DGRAD: Cout, Cin_g, groups, fold_mod, T, rows (ECs|OCs), cols (CoutW|EW), E
+  // CONVT_FUSED: Cin, Cout, KX, KY, KZ, sx, sy, sz, ICs, CoutW
+  // CONVT_PHASE: Cin, Cout, KX, KY, KZ, sx, sy, sz, px, py, pz, Jx, Jy, Jz, ICs, CoutW
+  // CONVT_DGRAD: Cin, Cout, T, UCs, CinW
+  int p[16];
+};
+constexpr int kPrepBatch = 12;
+int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n, hipStream_t s);
+
 // Loss / optimizer (loss_adam.hip)
 int launch_loss_pixel(const float *pred, int B, int C, int PX, int PY, int PZ,
                       const void *mask, int mask_dtype, const void *pwl,

@@ -557,19 +557,33 @@ int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R, hip
   return 0;
 }
 
-__global__ void __launch_bounds__(256)
-reduce_partials_kernel(const float *part, int R, int W, int n, float *out, int accumulate) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
+// Fixed-order fp64 sum of one column of the partial rows: one workgroup per
+// output element j, 256 threads stride over the R rows, then an LDS tree.
+__device__ __forceinline__ double block_sum_column(const float *part, int R, int W, int j) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
   double s = 0.0;
-  for (int r = 0; r < R; ++r) s += (double)part[(size_t)r * W + j];
-  out[j] = accumulate ? out[j] + (float)s : (float)s;
+  for (int r = tid; r < R; r += 256) s += (double)part[(size_t)r * W + j];
+  red[tid] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  return red[0];
+}
+
+__global__ void __launch_bounds__(256)
+reduce_partials_kernel(const float *part, int R, int W, float *out, int accumulate) {
+  const int j = blockIdx.x;
+  const double s = block_sum_column(part, R, W, j);
+  if (threadIdx.x == 0) out[j] = accumulate ? out[j] + (float)s : (float)s;
 }
 
 int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
                            int accumulate, hipStream_t s) {
-  HCU_TIMED(s, "reduce_partials_kernel", 0.0, 0.0, hipLaunchKernelGGL(reduce_partials_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part, R,
-                     W, n, out, accumulate));
+  HCU_TIMED(s, "reduce_partials_kernel", 0.0, 0.0, hipLaunchKernelGGL(reduce_partials_kernel, dim3(n), dim3(256), 0, s, part, R,
+                     W, out, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -787,13 +801,13 @@ int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T,
   return 0;
 }
 
-// out_conv weight/bias gradient from the fused backward's partial rows.
+// out_conv weight/bias gradient from the fused backward's partial rows
+// (one workgroup per dw/db element).
 __global__ void __launch_bounds__(256)
 outconv_wfinalize_kernel(const float *part, int R, int Co, int C, int Cs, float *dw, float *db,
                          int accumulate) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int j = blockIdx.x;
   const int W = Co * Cs + Co;
-  if (j >= Co * C + Co) return;
   int src;
   float *dst;
   if (j < Co * C) {
@@ -804,15 +818,14 @@ outconv_wfinalize_kernel(const float *part, int R, int Co, int C, int Cs, float 
     src = Co * Cs + (j - Co * C);
     dst = db + (j - Co * C);
   }
-  double s = 0.0;
-  for (int r = 0; r < R; ++r) s += (double)part[(size_t)r * W + src];
-  *dst = accumulate ? *dst + (float)s : (float)s;
+  const double s = block_sum_column(part, R, W, src);
+  if (threadIdx.x == 0) *dst = accumulate ? *dst + (float)s : (float)s;
 }
 
 int launch_outconv_wfinalize(const float *part_oc, int R, int Co, int C, int Cs, float *dw,
                              float *db, int accumulate, hipStream_t s) {
   const int n = Co * C + Co;
-  HCU_TIMED(s, "outconv_wfinalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_wfinalize_kernel, dim3((n + 255) / 256), dim3(256), 0, s, part_oc,
+  HCU_TIMED(s, "outconv_wfinalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_wfinalize_kernel, dim3(n), dim3(256), 0, s, part_oc,
                      R, Co, C, Cs, dw, db, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;

@@ -1,0 +1,124 @@
+// All weight re-layouts of one network step in a few launches (one workgroup
+// row per job) instead of one launch per layer: the executor prepares every
+// conv / convT weight once at the start of forward into the `saved`
+// workspace, and forward and backward read the prepared images from there.
+// Element i of a job is exactly what the per-layer prep_* kernel in
+// pointwise.hip writes for that layer (same index decoding, same values).
+#include "common.h"
+#include "timing.h"
+#include <algorithm>
+
+namespace hcu {
+
+struct PrepBatch {
+  int n;
+  PrepJob j[kPrepBatch];
+};
+
+__device__ __forceinline__ bool prep_index2(const WPack &pk, int64_t i, int T, int ICs, int CoutW,
+                                            int &t, int &ci, int &co) {
+  if (pk.on) return wpack_decode(pk, i, T, t, ci, co);
+  co = (int)(i % CoutW);
+  const int64_t q = i / CoutW;
+  ci = (int)(q % ICs);
+  t = (int)(q / ICs);
+  return true;
+}
+
+// Effective (folded, block-diagonal) Conv3d weight element W_eff[o][e][t].
+__device__ __forceinline__ float weff2(const float *w, int o, int e, int t, int Cout, int Cin_g,
+                                       int groups, int fold_mod, int T) {
+  const int g = o / (Cout / groups);
+  const int cin_total = groups * Cin_g;
+  float s = 0.f;
+  for (int cp = e; cp < cin_total; cp += fold_mod) {
+    const int c = cp - g * Cin_g;
+    if (c >= 0 && c < Cin_g) s += w[((size_t)o * Cin_g + c) * T + t];
+  }
+  return s;
+}
+
+__device__ float prep_value(const PrepJob &jb, const float *w, int64_t i) {
+  const int *p = jb.p;
+  switch (jb.kind) {
+    case PREP_CONV_FWD: {
+      int t, e, co;
+      if (prep_index2(jb.pk, i, p[4], p[5], p[6], t, e, co) && co < p[0] && e < p[7])
+        return weff2(w, co, e, t, p[0], p[1], p[2], p[3], p[4]);
+      return 0.f;
+    }
+    case PREP_CONV_DGRAD: {
+      int tp, co, e;
+      if (prep_index2(jb.pk, i, p[4], p[5], p[6], tp, co, e) && co < p[0] && e < p[7])
+        return weff2(w, co, e, p[4] - 1 - tp, p[0], p[1], p[2], p[3], p[4]);
+      return 0.f;
+    }
+    case PREP_CONVT_FUSED: {
+      const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
+      const int sx = p[5], sy = p[6], sz = p[7];
+      const int Jx = KX / sx, Jy = KY / sy, Jz = KZ / sz;
+      const int T = Jx * Jy * Jz;
+      int t, ci, nn;
+      if (prep_index2(jb.pk, i, T, p[8], p[9], t, ci, nn) && ci < Cin && nn < sx * sy * sz * Cout) {
+        const int ph = nn / Cout, co = nn % Cout;
+        const int qz = ph % sz, qy = (ph / sz) % sy, qx = ph / (sz * sy);
+        const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
+        const int kx = qx + sx * (Jx - 1 - tx), ky = qy + sy * (Jy - 1 - ty),
+                  kz = qz + sz * (Jz - 1 - tz);
+        return w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
+      }
+      return 0.f;
+    }
+    case PREP_CONVT_PHASE: {
+      const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
+      const int Jx = p[11], Jy = p[12], Jz = p[13], ICs = p[14], CoutW = p[15];
+      const int co = (int)(i % CoutW);
+      const int64_t q = i / CoutW;
+      const int ci = (int)(q % ICs);
+      const int t = (int)(q / ICs);
+      const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
+      const int kx = p[8] + p[5] * (Jx - 1 - tx), ky = p[9] + p[6] * (Jy - 1 - ty),
+                kz = p[10] + p[7] * (Jz - 1 - tz);
+      if (ci < Cin && co < Cout && kx < KX && ky < KY && kz < KZ)
+        return w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
+      return 0.f;
+    }
+    default: {  // PREP_CONVT_DGRAD
+      int t, co, ci;
+      if (prep_index2(jb.pk, i, p[2], p[3], p[4], t, co, ci) && ci < p[0] && co < p[1])
+        return w[((size_t)ci * p[1] + co) * p[2] + t];
+      return 0.f;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
+  const PrepJob &jb = b.j[blockIdx.y];
+  const float *w = params + jb.src;
+  float *dst = dst_base + jb.dst;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < jb.n;
+       i += (int64_t)gridDim.x * 256)
+    dst[i] = prep_value(jb, w, i);
+}
+
+int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n,
+                    hipStream_t s) {
+  for (int j0 = 0; j0 < n; j0 += kPrepBatch) {
+    PrepBatch b{};
+    b.n = std::min(kPrepBatch, n - j0);
+    int64_t most = 1;
+    for (int k = 0; k < b.n; ++k) {
+      b.j[k] = jobs[j0 + k];
+      most = std::max(most, b.j[k].n);
+    }
+    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((most + 255) / 256, 128));
+    HCU_TIMED(s, "prep_all_kernel", 0.0, 0.0,
+              hipLaunchKernelGGL(prep_all_kernel, dim3(gx, b.n), dim3(256), 0, s, params,
+                                 dst_base, b));
+    HCU_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace hcu

@@ -87,6 +87,7 @@ struct ConvLayer {
   WGradArgs wg{};
   BNLayer bn;
   size_t y_off = 0;
+  size_t wf_off = 0, wd_off = 0;  // prepared fwd / dgrad weight images in `saved`
 };
 
 struct ConvTLayer {
@@ -102,6 +103,8 @@ struct ConvTLayer {
   GConvArgs dgrad{};
   WGradArgs wg{};
   size_t u_off = 0;
+  size_t wf_off = 0, wd_off = 0;   // prepared weights in `saved` (fused fwd, dgrad)
+  std::vector<size_t> wph_off;     // per-phase fwd weights when not fused
 };
 
 BNCoef coef_at(char *saved, const BNLayer &bn) {
@@ -309,6 +312,7 @@ struct hcu_unet_plan {
   Dims outd;
   int64_t n_params = 0;
   int n_bn = 0;
+  std::vector<PrepJob> prep_jobs;  // weight re-layouts, one batched launch per forward
   size_t saved_bytes = 0, scratch_bytes = 0;
   // scratch layout
   size_t buf_off[2] = {0, 0};
@@ -464,6 +468,56 @@ int build_plan(hcu_unet_plan &p) {
     const int R = outconv_bwd_rows(cur.vox(), cur.Cs);
     p.max_part = std::max(p.max_part, (size_t)R * cur.Cs * 2 + (size_t)R * (p.Co * cur.Cs + p.Co) + 64);
   }
+  // Prepared (GEMM-layout) weights of every layer: written once per forward by
+  // one batched launch, read by the forward and backward GEMMs.
+  p.prep_jobs.clear();
+  auto add_job = [&](int kind, size_t n, int64_t src, const WPack &pk, const int *prm, int np,
+                     size_t &off) {
+    PrepJob j{};
+    j.kind = kind;
+    j.n = (int64_t)n;
+    j.src = src;
+    off = saved.take_floats(n);
+    j.dst = (int64_t)(off / sizeof(float));
+    j.pk = pk;
+    std::copy(prm, prm + np, j.p);
+    p.prep_jobs.push_back(j);
+  };
+  auto conv_jobs = [&](ConvLayer &cl) {
+    const int pf[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.fwd.ICs, cl.fwd.CoutW,
+                       std::min(cl.fold_mod, cl.groups * cl.Cin_g)};
+    add_job(PREP_CONV_FWD, prep_floats_fwd(cl), cl.w_off, wpack_of(cl.fwd), pf, 8, cl.wf_off);
+    const int pd[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.dgrad.ICs,
+                       cl.dgrad.CoutW, cl.E};
+    add_job(PREP_CONV_DGRAD, prep_floats_dgrad(cl), cl.w_off, wpack_of(cl.dgrad), pd, 8,
+            cl.wd_off);
+  };
+  for (int i = 0; i < L; ++i) {
+    conv_jobs(p.dc1[i]);
+    conv_jobs(p.dc2[i]);
+  }
+  for (int j = 0; j + 1 < L; ++j) {
+    ConvTLayer &u = p.up[j];
+    conv_jobs(p.uc1[j]);
+    conv_jobs(p.uc2[j]);
+    if (u.fused) {
+      const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
+                          u.fwdf.ICs, u.fwdf.CoutW};
+      add_job(PREP_CONVT_FUSED, wprep_floats(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 10, u.wf_off);
+    } else {
+      u.wph_off.assign(u.phases.size(), 0);
+      for (size_t ph = 0; ph < u.phases.size(); ++ph) {
+        const int *pj = &u.pJ[ph * 6];
+        const GConvArgs &a = u.phases[ph];
+        const int pf[16] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
+                            pj[0], pj[1], pj[2], pj[3], pj[4], pj[5], a.ICs, a.CoutW};
+        add_job(PREP_CONVT_PHASE, (size_t)pj[3] * pj[4] * pj[5] * a.ICs * a.CoutW, u.w_off,
+                WPack{}, pf, 16, u.wph_off[ph]);
+      }
+    }
+    const int pd[5] = {u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW};
+    add_job(PREP_CONVT_DGRAD, wprep_floats(u.dgrad), u.w_off, wpack_of(u.dgrad), pd, 5, u.wd_off);
+  }
   p.saved_bytes = saved.off;
 
   Region scratch;
@@ -498,14 +552,11 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
                  const float *ish, int training) {
   HCU_HIP(hipGetLastError());
   tag(L.name, "fwd");
-  if (int e = launch_prep_conv_fwd(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups, L.fold_mod,
-                                   L.T, L.fwd.ICs, L.fwd.CoutW, wpack_of(L.fwd), c.s))
-    return e;
   GConvArgs a = L.fwd;
   a.in = in;
   a.in_scale = isc;
   a.in_shift = ish;
-  a.w = c.wprep();
+  a.w = c.fptr(c.sv, L.wf_off);
   a.bias = c.P + L.b_off;
   a.out = c.fptr(c.sv, L.y_off);
   a.stats = training ? c.part() : nullptr;
@@ -548,13 +599,9 @@ int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float 
   if (int e = launch_wgrad_finalize(f, c.s)) return e;
   if (!dA) return 0;
   tag(L.name, "dgrad");
-  if (int e = launch_prep_conv_dgrad(c.P + L.w_off, c.wprep(), L.Cout, L.Cin_g, L.groups,
-                                     L.fold_mod, L.T, L.dgrad.ICs, L.dgrad.CoutW, L.E,
-                                     wpack_of(L.dgrad), c.s))
-    return e;
   GConvArgs a = L.dgrad;
   a.in = dy;
-  a.w = c.wprep();
+  a.w = c.fptr(c.sv, L.wd_off);
   a.out = dA;
   a.partial = c.kpart();
   return launch_conv_any(a, c.s);
@@ -646,6 +693,10 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   float *xcl = c.fptr(c.sv, p.xcl_off);
   tag(std::string("in"), "fwd");
   if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
+  tag(std::string("prep"), "fwd");
+  if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_jobs.data(),
+                              (int)p.prep_jobs.size(), c.s))
+    return e;
   const float *src = xcl;
   const float *ssc = nullptr, *ssh = nullptr;
   for (int i = 0; i < p.L; ++i) {
@@ -675,14 +726,10 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
     float *U = c.fptr(c.sv, u.u_off);
     if (u.fused) {
       GConvArgs a = u.fwdf;
-      if (int e = launch_prep_convt_fused(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.K[0], u.K[1],
-                                          u.K[2], u.S[0], u.S[1], u.S[2], a.ICs, a.CoutW,
-                                          wpack_of(a), c.s))
-        return e;
       a.in = src;
       a.in_scale = ssc;
       a.in_shift = ssh;
-      a.w = c.wprep();
+      a.w = c.fptr(c.sv, u.wf_off);
       a.bias = c.P + u.b_off;
       a.out = U;
       a.stats = nullptr;
@@ -690,16 +737,11 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
       if (int e = launch_conv_any(a, c.s)) return e;
     }
     for (size_t ph = 0; !u.fused && ph < u.phases.size(); ++ph) {
-      const int *pj = &u.pJ[ph * 6];
       GConvArgs a = u.phases[ph];
-      if (int e = launch_prep_convt_fwd(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.K[0], u.K[1],
-                                        u.K[2], u.S[0], u.S[1], u.S[2], pj[0], pj[1], pj[2],
-                                        pj[3], pj[4], pj[5], a.ICs, a.CoutW, c.s))
-        return e;
       a.in = src;
       a.in_scale = ssc;
       a.in_shift = ssh;
-      a.w = c.wprep();
+      a.w = c.fptr(c.sv, u.wph_off[ph]);
       a.bias = c.P + u.b_off;
       a.out = U;
       a.stats = nullptr;
@@ -805,13 +847,10 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
       if (int e = launch_wgrad_finalize(f, c.s)) return e;
     }
     tag(u.name, "dgrad");
-    if (int e = launch_prep_convt_dgrad(c.P + u.w_off, c.wprep(), u.Cin, u.Cout, u.T, u.dgrad.ICs,
-                                        u.dgrad.CoutW, wpack_of(u.dgrad), c.s))
-      return e;
     {
       GConvArgs a = u.dgrad;
       a.in = A;
-      a.w = c.wprep();
+      a.w = c.fptr(c.sv, u.wd_off);
       a.out = Bf;
       a.partial = c.kpart();
       if (int e = launch_conv_any(a, c.s)) return e;
