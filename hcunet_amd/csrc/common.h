@@ -88,6 +88,11 @@ struct GConvArgs {
   int epi_lds, nc4, areg;             // conv2 epilogue through LDS (float4 stores), float4
                                       // groups, floats of the halo / C-tile LDS region
   FastDiv fNT, fNTZ, fNTY;            // tile index decomposition
+  // conv8 (conv8.hip): <= 8 output channels on the 16-block 4x4x1 MFMA
+  int use_conv8, G8, HVP;             // enabled, 32-voxel groups per wave, halo plane stride
+  FastDiv fKZ, fKY;                   // tap index decomposition (conv8 K loop)
+  int dbg;                            // ablation bits (HCU_CONV8_DBG; 0 in production)
+  int HZr, MZ;                        // conv8: loaded halo z extent, z stride of the M rows
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 // Chooses the tile and kernel variant; returns 0 or an error code.
@@ -97,25 +102,36 @@ int plan_conv2(GConvArgs &a, int target_blocks);
 int launch_conv2(const GConvArgs &a, hipStream_t s);
 size_t conv2_partial_floats(const GConvArgs &a);
 int conv2_stat_rows(const GConvArgs &a);
+int plan_conv8(GConvArgs &a, int target_blocks);
+int launch_conv8(const GConvArgs &a, hipStream_t s);
 // Plans conv2 when it supports the shape, else the generic gconv.
 bool conv2_disabled();   // HCU_NO_CONV2=1 forces the generic kernel (A/B testing)
 inline int plan_conv_any(GConvArgs &a, int target_blocks) {
+  GConvArgs b8 = a;
+  if (plan_conv8(b8, target_blocks) == 0) {
+    a = b8;
+    return 0;
+  }
   GConvArgs b = a;
+  b.use_conv8 = 0;
   if (!conv2_disabled() && plan_conv2(b, target_blocks) == 0) {
     a = b;
     return 0;
   }
   a.use_conv2 = 0;
+  a.use_conv8 = 0;
   return plan_gconv(a, target_blocks);
 }
 inline int launch_conv_any(const GConvArgs &a, hipStream_t s) {
+  if (a.use_conv8) return launch_conv8(a, s);
   return a.use_conv2 ? launch_conv2(a, s) : launch_gconv(a, s);
 }
 inline int gconv_rows(const GConvArgs &a) {
+  if (a.use_conv8) return a.gridx;
   return a.use_conv2 ? conv2_stat_rows(a) : a.B * a.ntx * a.nty * a.ntz;
 }
 inline size_t conv_partial_floats(const GConvArgs &a) {
-  return a.use_conv2 ? conv2_partial_floats(a) : 0;
+  return (a.use_conv2 && !a.use_conv8) ? conv2_partial_floats(a) : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -240,11 +256,20 @@ int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V,
 // lane group g and component j as conv2_kernel consumes them (tap t =
 // s*TPS + g/(CK/4), ci = chunk*CK + 4*(g % (CK/4)) + j, TPS = 16/CK); taps
 // t >= T in the last step are zero.
+// on == 2: the conv8 layout wg[t][ci/4][co (8)][ci%4] (CK = ICs/4, S = T).
 struct WPack {
   int on, CK, S, ICs, CoutW;
 };
 inline WPack wpack_of(const GConvArgs &a) {
   WPack p{};
+  if (a.use_conv8) {
+    p.on = 2;
+    p.CK = a.ICs / 4;
+    p.S = a.KX * a.KY * a.KZ;
+    p.ICs = a.ICs;
+    p.CoutW = 8;
+    return p;
+  }
   if (!a.use_conv2) return p;
   const int T = a.KX * a.KY * a.KZ, TPS = 16 / a.CK;
   p.on = 1;
@@ -255,8 +280,15 @@ inline WPack wpack_of(const GConvArgs &a) {
   return p;
 }
 // Floats of the prepared weight buffer of a GEMM planned in `a`.
+// Elements of a prepared weight buffer (plain [T][ICs][CoutW] when !on).
+__host__ __device__ inline int64_t wpack_count(const WPack &p, int T, int ICs, int CoutW) {
+  if (p.on == 2) return (int64_t)p.S * p.CK * 32;
+  if (p.on) return (int64_t)p.ICs * p.S * (16 / p.CK) * p.CoutW;
+  return (int64_t)T * ICs * CoutW;
+}
 inline size_t wprep_floats(const GConvArgs &a) {
   const int T = a.KX * a.KY * a.KZ;
+  if (a.use_conv8) return (size_t)T * a.ICs * 8;
   if (!a.use_conv2) return (size_t)T * a.ICs * a.CoutW;
   const WPack p = wpack_of(a);
   return (size_t)a.ICs * p.S * (16 / p.CK) * a.CoutW;
@@ -264,6 +296,14 @@ inline size_t wprep_floats(const GConvArgs &a) {
 // Packed index -> (t, ci, co); false for a padded tap.
 __device__ __forceinline__ bool wpack_decode(const WPack &p, int64_t i, int T, int &t, int &ci,
                                              int &co) {
+  if (p.on == 2) {
+    const int j = (int)(i & 3);
+    co = (int)((i >> 2) & 7);
+    const int q = (int)(i >> 5);
+    ci = (q % p.CK) * 4 + j;
+    t = q / p.CK;
+    return t < T;
+  }
   const int j = (int)(i & 3);
   int64_t q = i >> 2;
   co = (int)(q % p.CoutW);

@@ -1,0 +1,400 @@
+// Implicit-GEMM convolution for layers with at most 8 output channels, on the
+// 16-block fp32 MFMA v_mfma_f32_4x4x1_16b_f32.
+//
+// The 16x16x4 form pads an 8-channel N to 16, so half of its work is zeros on
+// the 8-channel level of the U-Net (the 256x256 level: the largest tensors of
+// the step).  Here block b of one instruction is (voxel group vg = b & 7,
+// channel group cg = b >> 3): one instruction covers 32 voxels x 8 channels x
+// one K element with no padding, at the same FLOP rate (tools/mfma_probe.hip:
+// 122 TF/s vs 129 TF/s for 16x16x4 on an issue-bound loop).
+//
+// Lane layout (probed): A lane l feeds row l&3 of block l>>2, B lane l feeds
+// column l&3 of block l>>2, result register r of lane l is (row r, column
+// l&3) of block l>>2.  So lane l carries voxel l&31 of its 32-voxel group as
+// A operand, output channel col = 4*(l>>5) + (l&3) as B operand, and holds the
+// results of voxels 4*((l>>2)&7) + r of that group for channel col.
+//
+// K = (tap, input channel).  A K-step (tap t, channels 4q..4q+3) is one
+// ds_read_b128 per lane from the halo image (4-channel planes [C4][HVP][4]:
+// 16 consecutive voxels of a plane cover the 64 banks, conflict-free) and one
+// ds_read_b128 of the packed weights [T][C4][8][4] (broadcast); component j
+// feeds MFMA j.  A wave owns G groups (32*G voxels), so each weight read is
+// shared by G groups: per K-step 1 + G b128 reads feed 4*G MFMAs.
+//
+// Persistent over output tiles (TX x TY x TZ voxels, TZ = the whole Z extent
+// up to 16); BatchNorm+ReLU of the producer applied while staging the halo;
+// bias, store and the BatchNorm partial statistics (one row per workgroup) in
+// the epilogue, straight from the accumulators.  Stride-1 Conv3d forward and
+// input gradient (hcat/unet.py:246-257 on the 8-channel level).
+#include "common.h"
+#include "timing.h"
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
+namespace hcu {
+
+bool conv8_disabled() {   // HCU_NO_CONV8=1 keeps the 16x16x4 kernels (A/B testing)
+  static const bool off = [] {
+    const char *e = getenv("HCU_NO_CONV8");
+    return e && e[0] == '1';
+  }();
+  return off;
+}
+
+template <int C4, int G, int NPF>
+__global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = a.KX * a.KY * a.KZ;
+  const int HZ = a.HZ, HYZ = a.HY * a.HZ, HV = a.HX * HYZ, HVP = a.HVP;
+  const int MT = a.TX * a.TY * a.MZ;   // M rows: z stride MZ (>= TZ; rows with lz >= TZ are idle)
+  float *alds = smem;                                            // [C4][HVP][4]
+  float *wlds = smem + (size_t)C4 * HVP * 4;                     // [T][C4][8][4]
+  int *toffs = reinterpret_cast<int *>(wlds + T * C4 * 32);      // [T] float offsets
+  int *rowoff = toffs + T;                                       // [128*G] store offsets, -1 past MT
+  int *rowpk = rowoff + 128 * G;                                  // [128*G] packed (lx,ly,lz)
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+
+  for (int i = tid; i < T * C4 * 8; i += 256)
+    reinterpret_cast<float4 *>(wlds)[i] = reinterpret_cast<const float4 *>(a.w)[i];
+  for (int t = tid; t < T; t += 256) {
+    const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
+    toffs[t] = (kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz) * 4;
+  }
+  for (int m = tid; m < 128 * G; m += 256) {
+    int q, lz, lx, ly;
+    a.fTZ.divmod(m, q, lz);
+    a.fTY.divmod(q, lx, ly);
+    const bool valid = m < MT && lz < a.TZ;
+    rowoff[m] = valid ? ((lx * a.SY + ly) * a.SZ + lz) * a.OCs : -1;
+    rowpk[m] = valid ? (lx << 20) | (ly << 10) | lz : (1023 << 20);
+  }
+  // A rows of this lane: voxel (wave*G + g)*32 + (lane & 31) of the tile
+  int vb[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int m = (wave * G + g) * 32 + (lane & 31);
+    int v = 0;
+    if (m < MT) {
+      int q, lz, lx, ly;
+      a.fTZ.divmod(m, q, lz);
+      a.fTY.divmod(q, lx, ly);
+      v = lx * HYZ + ly * HZ + lz;
+    }
+    vb[g] = v * 4;
+  }
+  const int col = ((lane >> 5) << 2) | (lane & 3);
+  const int wcol = col * 4;
+  const bool cstore = col < a.OCs, cstat = col < a.Cout;
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.out, 0, a.B * a.SX * a.SY * a.SZ * a.OCs * 4, 0x00020000);
+  const float bias = (a.bias && cstat) ? a.bias[col] : 0.f;
+  float s1 = 0.f, s2 = 0.f;
+  const bool act = a.in_scale != nullptr;
+  const int S = T * C4;
+
+  // Tap offsets are wave-uniform scalar arithmetic (no LDS read in the address
+  // chain, so waiting for a step's fragments never drains the next step's).
+  const int tdx = a.dx * HYZ * 4, tdy = a.dy * HZ * 4, tdz = a.dz * 4;
+  auto load = [&](int s, floatx4 &bw, floatx4 (&av)[G]) {
+    const int t = s / C4, q = s - t * C4;
+    int t1, kz, kx, ky;
+    a.fKZ.divmod(t, t1, kz);
+    a.fKY.divmod(t1, kx, ky);
+    bw = *reinterpret_cast<const floatx4 *>(wlds + s * 32 + wcol);
+    const float *ap = alds + (size_t)q * HVP * 4 + kx * tdx + ky * tdy + kz * tdz;
+#pragma unroll
+    for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const floatx4 *>(ap + vb[g]);
+  };
+
+  // Halo staging: thread tid always handles elements idx = tid + u*256 (channel
+  // quad idx % C4 of halo voxel idx / C4); their halo coordinates are the same
+  // for every tile, so they are decoded once.  The next tile's elements are
+  // loaded into registers while the current tile's MFMAs run.
+  int hpk[NPF];
+#pragma unroll
+  for (int u = 0; u < NPF; ++u) {
+    const int idx = tid + u * 256;
+    hpk[u] = -1;
+    if (idx < HV * C4) {
+      const int v = idx / C4;
+      int t2, hz, hx, hy;
+      a.fHZ.divmod(v, t2, hz);
+      a.fHY.divmod(t2, hx, hy);
+      hpk[u] = (hx << 20) | (hy << 10) | hz;
+    }
+  }
+  const int cq = (tid % C4) * 4;   // idx % C4 == tid % C4 since 256 % C4 == 0
+  const float4 sc = act ? *reinterpret_cast<const float4 *>(a.in_scale + cq)
+                        : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 sh = act ? *reinterpret_cast<const float4 *>(a.in_shift + cq)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+  // Halo loads go through a buffer descriptor of the tile's batch sample: an
+  // element outside the input gets an out-of-range offset, which the hardware
+  // range check turns into 0 (no branch per element); BatchNorm+ReLU is
+  // applied when the element is written to LDS, selected to 0 outside.
+  const uint32_t bX = (uint32_t)a.IY * a.IZ * a.ICs * 4, bY = (uint32_t)a.IZ * a.ICs * 4,
+                 bZ = (uint32_t)a.ICs * 4;
+  const int sample_bytes = a.IX * a.IY * a.IZ * a.ICs * 4;
+  floatx4 pf[NPF];
+  uint32_t okbits = 0;
+  auto fetch = [&](int tile) {
+    int b, r, tzi, tyi, txi;
+    a.fNT.divmod(tile, b, r);
+    a.fNTZ.divmod(r, r, tzi);
+    a.fNTY.divmod(r, txi, tyi);
+    const int gx0 = txi * a.TX - a.px, gy0 = tyi * a.TY - a.py, gz0 = tzi * a.TZ - a.pz;
+    const bool inb = gx0 >= 0 && gy0 >= 0 && gz0 >= 0 && gx0 + a.HX <= a.IX &&
+                     gy0 + a.HY <= a.IY && gz0 + a.HZr <= a.IZ;
+    const float *bp = a.in + (size_t)b * a.IX * a.IY * a.IZ * a.ICs;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, (a.dbg & 2) ? 0 : sample_bytes, 0x00020000);
+    const int base_off = gx0 * (int)bX + gy0 * (int)bY + gz0 * (int)bZ + cq * 4;
+    okbits = 0;
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int hp = hpk[u];
+      const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
+      const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+      const bool ok = hp >= 0 && hz < a.HZr && (inb || ((unsigned)gx < (unsigned)a.IX &&
+                                          (unsigned)gy < (unsigned)a.IY &&
+                                          (unsigned)gz < (unsigned)a.IZ));
+      const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
+                         : 0x7ffffff0;
+      pf[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      okbits |= (ok ? 1u : 0u) << u;
+    }
+  };
+  if (blockIdx.x < total) fetch(blockIdx.x);
+  if (a.dbg & 32) return;
+
+  for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    int b, r, tzi, tyi, txi;
+    a.fNT.divmod(tile, b, r);
+    a.fNTZ.divmod(r, r, tzi);
+    a.fNTY.divmod(r, txi, tyi);
+    const int ox0 = txi * a.TX, oy0 = tyi * a.TY, oz0 = tzi * a.TZ;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NPF; ++u) {
+      const int idx = tid + u * 256;
+      floatx4 v = pf[u];
+      if (act) {
+        v[0] = fmaxf(fmaf(v[0], sc.x, sh.x), 0.f);
+        v[1] = fmaxf(fmaf(v[1], sc.y, sh.y), 0.f);
+        v[2] = fmaxf(fmaf(v[2], sc.z, sh.z), 0.f);
+        v[3] = fmaxf(fmaf(v[3], sc.w, sh.w), 0.f);
+      }
+      const bool ok = (okbits >> u) & 1u;
+      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+      // elements past the halo write the unused last slot of the last plane
+      const int slot = hpk[u] >= 0 ? (idx % C4) * HVP + idx / C4 : C4 * HVP - 1;
+      if (!(a.dbg & 16)) *reinterpret_cast<floatx4 *>(alds + (size_t)slot * 4) = ok ? v : z;
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < total) fetch(tile + gridDim.x);
+    // ---- MFMA over the K-steps, next step's fragments loaded ahead
+    floatx4 acc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 b0, b1, a0[G], a1[G];
+    load(0, b0, a0);
+    for (int s = 0; s < ((a.dbg & 1) ? 0 : S); s += 2) {
+      load(min(s + 1, S - 1), b1, a1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(a0[g][c], b0[c], acc[g], 0, 0, 0);
+      load(min(s + 2, S - 1), b0, a0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < S) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+            acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(a1[g][c], b1[c], acc[g], 0, 0, 0);
+      }
+    }
+    // ---- epilogue: bias, store, BatchNorm partial statistics.  The store
+    // offsets are read from LDS up front (one wait), and the output pointer is
+    // a global-address-space pointer so the stores cannot alias LDS and do not
+    // serialise the table reads.
+    const int tbase = ((((b * a.SX + ox0) * a.SY + oy0) * a.SZ + oz0) * a.OCs + col) * 4;
+    const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
+    int ro[G * 4];
+    const int mb = wave * G * 32 + ((lane >> 2) & 7) * 4;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) ro[g * 4 + rr] = rowoff[mb + g * 32 + rr];
+    if (!interior) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int pk = rowpk[mb + g * 32 + rr];
+          const bool in = ox0 + (pk >> 20) < a.OX && oy0 + ((pk >> 10) & 1023) < a.OY &&
+                          oz0 + (pk & 1023) < a.OZ;
+          ro[g * 4 + rr] = in ? ro[g * 4 + rr] : -1;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < ((a.dbg & 8) ? 0 : G); ++g) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int o = ro[g * 4 + rr];
+        const float v = acc[g][rr] + bias;
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_bit_cast(uint32_t, v), ors,
+            (o >= 0 && cstore && !(a.dbg & 4)) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
+        const float w = (o >= 0 && cstat) ? v : 0.f;
+        s1 += w;
+        s2 = fmaf(w, w, s2);
+      }
+    }
+  }
+  if (!a.stats) return;
+  // lanes sharing a channel differ in lane bits 2..4: fixed-order butterfly
+  s1 += __shfl_xor(s1, 4);
+  s2 += __shfl_xor(s2, 4);
+  s1 += __shfl_xor(s1, 8);
+  s2 += __shfl_xor(s2, 8);
+  s1 += __shfl_xor(s1, 16);
+  s2 += __shfl_xor(s2, 16);
+  __syncthreads();
+  float *red = smem;  // [4 waves][8 channels][2]
+  if (((lane >> 2) & 7) == 0) {
+    red[(wave * 8 + col) * 2 + 0] = s1;
+    red[(wave * 8 + col) * 2 + 1] = s2;
+  }
+  __syncthreads();
+  if (tid < 8) {
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      t1 += red[(w * 8 + tid) * 2 + 0];
+      t2 += red[(w * 8 + tid) * 2 + 1];
+    }
+    a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 0] = t1;
+    a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 1] = t2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+static long conv8_lds(const GConvArgs &a, int C4, int HVP, int G) {
+  const int T = a.KX * a.KY * a.KZ;
+  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G) * 4;
+}
+
+// Chooses the tile, groups per wave and grid for conv8_kernel; non-zero when
+// the shape is not one conv8 handles (the caller then plans conv2 / gconv).
+int plan_conv8(GConvArgs &a, int target_blocks) {
+  a.use_conv8 = 0;
+  if (conv8_disabled()) return 1;
+  if (a.nph > 1 || a.sx != 1 || a.sy != 1 || a.sz != 1) return 1;
+  if (a.osx != 1 || a.osy != 1 || a.osz != 1 || a.ofx || a.ofy || a.ofz) return 1;
+  if (a.Cout > 8 || a.OCs > 8 || a.ICs % 4) return 1;
+  const int C4 = a.ICs / 4;
+  if (C4 != 1 && C4 != 2 && C4 != 4) return 1;
+  if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return 2;
+  const int ntz = cdiv(a.OZ, 16);
+  const int TZ = cdiv(a.OZ, ntz);
+  const int HZr = TZ + (a.KZ - 1) * a.dz;
+  // M rows with a z stride of 16 and a halo z stride of 16: the 16 lanes of a
+  // ds_read_b128 lane group then read 16 different banks (a z stride of 15
+  // puts two lanes of a group on one bank).  Only when it wastes <= 1/8.
+  const bool pad16 = false;  // measured slower (NPF grows); kept for reference: TZ >= 14 && HZr <= 16
+  const int MZ = pad16 ? 16 : TZ, HZS = pad16 ? 16 : HZr;
+  const int gs[3] = {8, 4, 2};
+  bool found = false;
+  for (int gi = 0; gi < 3; ++gi) {
+    const int G = gs[gi];
+    const int txy = std::max(1, 128 * G / MZ);
+    int TX = std::max(1, (int)std::floor(std::sqrt((double)txy)));
+    int TY = std::max(1, txy / TX);
+    TX = std::min(TX, a.OX);
+    TY = std::min(TY, a.OY);
+    const int HX = TX + (a.KX - 1) * a.dx, HY = TY + (a.KY - 1) * a.dy;
+    const int HV = HX * HY * HZS;
+    const int HVP = round_up(HV, 16) + 8;
+    const long lds = conv8_lds(a, C4, HVP, G);
+    const long tiles = (long)a.B * cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz;
+    if (lds > 80 * 1024 || HV * C4 > 16 * 256) continue;
+    a.G8 = G;
+    a.TX = TX;
+    a.TY = TY;
+    a.TZ = TZ;
+    a.MZ = MZ;
+    a.HX = HX;
+    a.HY = HY;
+    a.HZ = HZS;
+    a.HZr = HZr;
+    a.HVP = HVP;
+    a.NPF = HV * C4 <= 8 * 256 ? 8 : (HV * C4 <= 12 * 256 ? 12 : 16);
+    a.lds_bytes = (int)std::max(lds, 4L * 8 * 2 * 4);
+    found = true;
+    if (tiles >= target_blocks / 2) break;
+  }
+  if (!found) return 4;
+  a.ntx = cdiv(a.OX, a.TX);
+  a.nty = cdiv(a.OY, a.TY);
+  a.ntz = ntz;
+  a.CK = a.ICs;
+  a.CoutW = 8;
+  a.NSUB = 1;
+  a.MPW = 1;
+  a.ksplit = 1;
+  a.cps = 1;
+  a.slice_floats = 0;
+  a.fHZ = FastDiv(a.HZ);
+  a.fHY = FastDiv(a.HY);
+  a.fTZ = FastDiv(a.MZ);   // M-row decomposition (z stride MZ)
+  a.fTY = FastDiv(a.TY);
+  a.fNT = FastDiv(a.ntx * a.nty * a.ntz);
+  a.fNTZ = FastDiv(a.ntz);
+  a.fNTY = FastDiv(a.nty);
+  a.fKZ = FastDiv(a.KZ);
+  {
+    const char *e = getenv("HCU_CONV8_DBG");
+    a.dbg = e ? atoi(e) : 0;
+  }
+  a.fKY = FastDiv(a.KY);
+  const long tiles = (long)a.B * a.ntx * a.nty * a.ntz;
+  const int occ = std::max(1, std::min(4, (int)(160 * 1024 / a.lds_bytes)));
+  a.gridx = (int)std::min<long>(tiles, 256L * occ);
+  a.use_conv8 = 1;
+  a.use_conv2 = 0;
+  return 0;
+}
+
+#define CONV8_CASE(C4_, G_, NPF_)                                                               \
+  if (C4 == C4_ && a.G8 == G_ && a.NPF == NPF_) {                                               \
+    HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ">", fl, by,                            \
+              hipLaunchKernelGGL((conv8_kernel<C4_, G_, NPF_>), dim3(a.gridx), dim3(256),       \
+                                 a.lds_bytes, s, a));                                           \
+    launched = true;                                                                            \
+  }
+#define CONV8_NPF(C4_, G_) \
+  CONV8_CASE(C4_, G_, 8) else CONV8_CASE(C4_, G_, 12) else CONV8_CASE(C4_, G_, 16)
+
+int launch_conv8(const GConvArgs &a, hipStream_t s) {
+  const int C4 = a.ICs / 4;
+  const double fl = a.flops > 0 ? a.flops
+                                : 2.0 * a.B * a.OX * a.OY * a.OZ * (double)a.Cout * a.KX * a.KY *
+                                      a.KZ * a.ICs;
+  const double by = 4.0 * ((double)a.B * a.IX * a.IY * a.IZ * a.ICs +
+                           (double)a.B * a.SX * a.SY * a.SZ * a.OCs);
+  bool launched = false;
+  CONV8_NPF(1, 8) else CONV8_NPF(1, 4) else CONV8_NPF(1, 2)
+  else CONV8_NPF(2, 8) else CONV8_NPF(2, 4) else CONV8_NPF(2, 2)
+  else CONV8_NPF(4, 8) else CONV8_NPF(4, 4) else CONV8_NPF(4, 2)
+  if (!launched) return fail(4, "conv8: unsupported variant");
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu

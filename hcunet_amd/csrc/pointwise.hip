@@ -650,7 +650,7 @@ __device__ inline float weff(const float *w, int o, int e, int t, int Cout, int 
 }
 
 __device__ __forceinline__ int64_t prep_count(const WPack &pk, int T, int ICs, int CoutW) {
-  return pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * ICs * CoutW;
+  return wpack_count(pk, T, ICs, CoutW);
 }
 // (t, ci, co) of element i of the prepared buffer (plain or packed layout).
 __device__ __forceinline__ bool prep_index(const WPack &pk, int64_t i, int T, int ICs, int CoutW,
@@ -680,7 +680,7 @@ prep_conv_fwd_kernel(const float *w, float *wg, int Cout, int Cin_g, int groups,
 int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int groups,
                          int fold_mod, int T, int ECs, int CoutW, WPack pk, hipStream_t s) {
   const int E = std::min(fold_mod, groups * Cin_g);
-  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * ECs * CoutW;
+  const int64_t n = wpack_count(pk, T, ECs, CoutW);
   HCU_TIMED(s, "prep_conv_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
                      Cin_g, groups, fold_mod, T, ECs, CoutW, E, pk));
   HCU_CHECK_LAUNCH();
@@ -704,7 +704,7 @@ prep_conv_dgrad_kernel(const float *w, float *wg, int Cout, int Cin_g, int group
 
 int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g, int groups,
                            int fold_mod, int T, int OCs, int EW, int E, WPack pk, hipStream_t s) {
-  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * OCs * EW;
+  const int64_t n = wpack_count(pk, T, OCs, EW);
   HCU_TIMED(s, "prep_conv_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
                      Cin_g, groups, fold_mod, T, OCs, EW, E, pk));
   HCU_CHECK_LAUNCH();
@@ -770,7 +770,7 @@ int launch_prep_convt_fused(const float *w, float *wg, int Cin, int Cout, int KX
                             int KZ, int sx, int sy, int sz, int ICs, int CoutW, WPack pk,
                             hipStream_t s) {
   const int T = (KX / sx) * (KY / sy) * (KZ / sz);
-  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * ICs * CoutW;
+  const int64_t n = wpack_count(pk, T, ICs, CoutW);
   HCU_TIMED(s, "prep_convt_fused_kernel", 0.0, 0.0,
             hipLaunchKernelGGL(prep_convt_fused_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg,
                                Cin, Cout, KX, KY, KZ, sx, sy, sz, ICs, CoutW, pk));
@@ -794,7 +794,7 @@ prep_convt_dgrad_kernel(const float *w, float *wg, int Cin, int Cout, int T, int
 
 int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
                             int CinW, WPack pk, hipStream_t s) {
-  const int64_t n = pk.on ? (int64_t)pk.ICs * pk.S * (16 / pk.CK) * pk.CoutW : (int64_t)T * UCs * CinW;
+  const int64_t n = wpack_count(pk, T, UCs, CinW);
   HCU_TIMED(s, "prep_convt_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
                      Cout, T, UCs, CinW, pk));
   HCU_CHECK_LAUNCH();
