@@ -93,6 +93,11 @@ struct GConvArgs {
   FastDiv fKZ, fKY;                   // tap index decomposition (conv8 K loop)
   int dbg;                            // ablation bits (HCU_CONV8_DBG; 0 in production)
   int HZr, MZ;                        // conv8: loaded halo z extent, z stride of the M rows
+  // dgrad epilogue fused with the BatchNorm+ReLU backward reduction of the
+  // layer whose output this gradient is for (bn_y = its pre-BN y, same layout
+  // as out): the stored value is dz = v * [y*scale+shift > 0] and the stats
+  // rows hold (sum dz, sum dz * (y-mean)*invstd) per channel.
+  const float *bn_y, *bn_scale, *bn_shift, *bn_mean, *bn_invstd;
   double flops;                       // algorithmic FLOPs (0: derive)
 };
 // Chooses the tile and kernel variant; returns 0 or an error code.
@@ -130,6 +135,8 @@ inline int gconv_rows(const GConvArgs &a) {
   if (a.use_conv8) return a.gridx;
   return a.use_conv2 ? conv2_stat_rows(a) : a.B * a.ntx * a.nty * a.ntz;
 }
+// Whether the kernel planned in `a` supports the fused BatchNorm-backward epilogue.
+inline bool conv_bnbwd_fusable(const GConvArgs &a) { return a.use_conv8 || a.use_conv2; }
 inline size_t conv_partial_floats(const GConvArgs &a) {
   return (a.use_conv2 && !a.use_conv8) ? conv2_partial_floats(a) : 0;
 }
@@ -203,7 +210,8 @@ int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
                            float *run_mean, float *run_var, int64_t *nbt,
                            float eps, float momentum, int training, BNCoef coef,
                            hipStream_t s);
-int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, double count,
+// part rows [R][W][2]; W = row stride in channels (>= Cs).
+int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, int W, double count,
                            BNCoef coef, float *dgamma, float *dbeta, int training,
                            int accumulate, hipStream_t s);
 
@@ -216,7 +224,8 @@ int bwd_rows(int64_t nvox, int Cs);
 int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef,
                                int64_t nvox, int Cs, float *part, int R,
                                hipStream_t s);
-// dz from a max-pool gradient dP (argmax recomputed from y).
+// dz from a max-pool gradient dP (argmax recomputed from y); R = pool_bwd_rows(...).
+int pool_bwd_rows(int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz);
 int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef,
                               float *dz, int B, int X, int Y, int Z, int Cs,
                               int kx, int ky, int kz, float *part, int R,

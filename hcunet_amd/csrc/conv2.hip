@@ -236,7 +236,18 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
 #pragma unroll
             for (int n = 0; n < NSUB; ++n) {
               if (coff[n] < 0) continue;
-              const float val = acc[j][n][r] + bias_v[n];
+              float val = acc[j][n][r] + bias_v[n];
+              if (a.bn_y && !split) {   // fused BatchNorm+ReLU backward (val = dA -> dz)
+                const int cc = coff[n] % a.OCs;
+                const float yv = a.bn_y[(vp - dst) + coff[n]];
+                val = fmaf(yv, a.bn_scale[cc], a.bn_shift[cc]) > 0.f ? val : 0.f;
+                vp[coff[n]] = val;
+                if (cst[n]) {
+                  s1[n] += val;
+                  s2[n] = fmaf(val, (yv - a.bn_mean[cc]) * a.bn_invstd[cc], s2[n]);
+                }
+                continue;
+              }
               vp[coff[n]] = val;
               if (cst[n]) {
                 s1[n] += val;
@@ -273,6 +284,14 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     bias4.w = cc + 3 < a.Cout ? a.bias[cc + 3] : 0.f;
   }
   float4 st1 = make_float4(0.f, 0.f, 0.f, 0.f), st2 = st1;
+  float4 bsc = st1, bsh = st1, bmu = st1, bis = st1;
+  if (a.bn_y && a.epi_lds) {
+    const int cc = n0 + ec4 * 4;
+    bsc = *reinterpret_cast<const float4 *>(a.bn_scale + cc);
+    bsh = *reinterpret_cast<const float4 *>(a.bn_shift + cc);
+    bmu = *reinterpret_cast<const float4 *>(a.bn_mean + cc);
+    bis = *reinterpret_cast<const float4 *>(a.bn_invstd + cc);
+  }
   auto epilogue_lds = [&](int b, int ox0, int oy0, int oz0) {
     __syncthreads();  // every wave is done reading the halo image
 #pragma unroll
@@ -303,6 +322,20 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
         v.y += bias4.y;
         v.z += bias4.z;
         v.w += bias4.w;
+        if (a.bn_y && !split) {   // fused BatchNorm+ReLU backward: v = dA -> dz, stats (dz, dz*xhat)
+          const float4 yv = *reinterpret_cast<const float4 *>(a.bn_y + ((tp - a.out) + rowoff[i]));
+          v.x = fmaf(yv.x, bsc.x, bsh.x) > 0.f ? v.x : 0.f;
+          v.y = fmaf(yv.y, bsc.y, bsh.y) > 0.f ? v.y : 0.f;
+          v.z = fmaf(yv.z, bsc.z, bsh.z) > 0.f ? v.z : 0.f;
+          v.w = fmaf(yv.w, bsc.w, bsh.w) > 0.f ? v.w : 0.f;
+          *reinterpret_cast<float4 *>(tp + rowoff[i]) = v;
+          st1.x += v.x; st1.y += v.y; st1.z += v.z; st1.w += v.w;
+          st2.x = fmaf(v.x, (yv.x - bmu.x) * bis.x, st2.x);
+          st2.y = fmaf(v.y, (yv.y - bmu.y) * bis.y, st2.y);
+          st2.z = fmaf(v.z, (yv.z - bmu.z) * bis.z, st2.z);
+          st2.w = fmaf(v.w, (yv.w - bmu.w) * bis.w, st2.w);
+          continue;
+        }
         *reinterpret_cast<float4 *>(tp + rowoff[i]) = v;
         st1.x += v.x; st1.y += v.y; st1.z += v.z; st1.w += v.w;
         st2.x = fmaf(v.x, v.x, st2.x);
@@ -512,6 +545,25 @@ __global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, in
     s.y += bv.y;
     s.z += bv.z;
     s.w += bv.w;
+    if (a.bn_y) {   // fused BatchNorm+ReLU backward: s = dA -> dz, stats (dz, dz*xhat)
+      const int c = c4 * 4;
+      const float4 yv = *reinterpret_cast<const float4 *>(a.bn_y + off);
+      const float4 sc = *reinterpret_cast<const float4 *>(a.bn_scale + c);
+      const float4 sh = *reinterpret_cast<const float4 *>(a.bn_shift + c);
+      const float4 mu = *reinterpret_cast<const float4 *>(a.bn_mean + c);
+      const float4 is = *reinterpret_cast<const float4 *>(a.bn_invstd + c);
+      s.x = fmaf(yv.x, sc.x, sh.x) > 0.f ? s.x : 0.f;
+      s.y = fmaf(yv.y, sc.y, sh.y) > 0.f ? s.y : 0.f;
+      s.z = fmaf(yv.z, sc.z, sh.z) > 0.f ? s.z : 0.f;
+      s.w = fmaf(yv.w, sc.w, sh.w) > 0.f ? s.w : 0.f;
+      *reinterpret_cast<float4 *>(a.out + off) = s;
+      st1[0] += s.x; st1[1] += s.y; st1[2] += s.z; st1[3] += s.w;
+      st2[0] = fmaf(s.x, (yv.x - mu.x) * is.x, st2[0]);
+      st2[1] = fmaf(s.y, (yv.y - mu.y) * is.y, st2[1]);
+      st2[2] = fmaf(s.z, (yv.z - mu.z) * is.z, st2[2]);
+      st2[3] = fmaf(s.w, (yv.w - mu.w) * is.w, st2[3]);
+      continue;
+    }
     *reinterpret_cast<float4 *>(a.out + off) = s;
     st1[0] += s.x; st1[1] += s.y; st1[2] += s.z; st1[3] += s.w;
     st2[0] = fmaf(s.x, s.x, st2[0]);
@@ -573,7 +625,14 @@ static long conv2_lds(const GConvArgs &a, int CK, int NT) {
 // Chooses CK / NSUB / MPW / tile / K split / prefetch depth / grid for
 // conv2_kernel.  Returns 0, or a non-zero code when conv2 cannot run this
 // shape (the caller then keeps gconv).
+static int env_int(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
 int plan_conv2(GConvArgs &a, int target_blocks) {
+  static const int mpw_target = env_int("HCU_CONV2_MPW_TARGET", 256);
+  static const int ks_target = env_int("HCU_CONV2_KS_TARGET", 256);
   if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return fail(2, "conv2: empty output grid");
   if (a.ICs % 4 != 0 || a.OCs % 4 != 0) return fail(1, "conv2: channel strides must be multiples of 4");
   if (a.nph < 1) a.nph = 1;
@@ -598,7 +657,7 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
     a.MPW = MPW;
     a.TX = TX;
     a.TY = TY;
-    if (blocks >= target_blocks) break;
+    if (blocks >= (mpw_target ? mpw_target : target_blocks)) break;
   }
   a.ntx = cdiv(a.OX, a.TX);
   a.nty = cdiv(a.OY, a.TY);
@@ -624,7 +683,7 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
   const int nchunks = a.ICs / a.CK;
   int ks = 1;
   if (256 % (a.OCs / 4) == 0)
-    while (ks < nchunks && tiles * nN * ks < target_blocks) ks *= 2;
+    while (ks < nchunks && tiles * nN * ks < (ks_target ? ks_target : target_blocks)) ks *= 2;
   ks = std::min(ks, nchunks);
   a.cps = cdiv(nchunks, ks);
   a.ksplit = cdiv(nchunks, a.cps);

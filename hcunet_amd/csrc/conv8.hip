@@ -90,6 +90,12 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   const bool cstore = col < a.OCs, cstat = col < a.Cout;
   const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
       (void *)a.out, 0, a.B * a.SX * a.SY * a.SZ * a.OCs * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)a.bn_y, 0, a.bn_y ? a.B * a.SX * a.SY * a.SZ * a.OCs * 4 : 0, 0x00020000);
+  const float bnsc = (a.bn_y && cstat) ? a.bn_scale[col] : 0.f;
+  const float bnsh = (a.bn_y && cstat) ? a.bn_shift[col] : 0.f;
+  const float bnmu = (a.bn_y && cstat) ? a.bn_mean[col] : 0.f;
+  const float bnis = (a.bn_y && cstat) ? a.bn_invstd[col] : 0.f;
   const float bias = (a.bias && cstat) ? a.bias[col] : 0.f;
   float s1 = 0.f, s2 = 0.f;
   const bool act = a.in_scale != nullptr;
@@ -247,13 +253,20 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int o = ro[g * 4 + rr];
-        const float v = acc[g][rr] + bias;
+        float v = acc[g][rr] + bias;
+        float w2 = v;
+        if (a.bn_y) {   // fused BatchNorm+ReLU backward: v = dA -> dz, stats (dz, dz*xhat)
+          const float yv = __builtin_bit_cast(
+              float, __builtin_amdgcn_raw_buffer_load_b32(yrs, o >= 0 ? tbase + o * 4 : 0x7ffffff0, 0, 0));
+          v = fmaf(yv, bnsc, bnsh) > 0.f ? v : 0.f;
+          w2 = (yv - bnmu) * bnis;
+        }
         __builtin_amdgcn_raw_buffer_store_b32(
             __builtin_bit_cast(uint32_t, v), ors,
             (o >= 0 && cstore && !(a.dbg & 4)) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
         const float w = (o >= 0 && cstat) ? v : 0.f;
         s1 += w;
-        s2 = fmaf(w, w, s2);
+        s2 = fmaf(w, w2, s2);
       }
     }
   }

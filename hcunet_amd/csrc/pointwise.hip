@@ -99,7 +99,7 @@ int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
 
 // BatchNorm backward finalisation: per channel sum dz and sum dz*xhat.
 __global__ void __launch_bounds__(256)
-bn_bwd_finalize_kernel(const float *part, int R, int C, int Cs, double count,
+bn_bwd_finalize_kernel(const float *part, int R, int C, int W, double count,
                        BNCoef coef, float *dgamma, float *dbeta, int training,
                        int accumulate) {
   __shared__ double r1[256], r2[256];
@@ -107,8 +107,8 @@ bn_bwd_finalize_kernel(const float *part, int R, int C, int Cs, double count,
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     for (int r = tid; r < R; r += 256) {
-      s1 += (double)part[((size_t)r * Cs + c) * 2 + 0];
-      s2 += (double)part[((size_t)r * Cs + c) * 2 + 1];
+      s1 += (double)part[((size_t)r * W + c) * 2 + 0];
+      s2 += (double)part[((size_t)r * W + c) * 2 + 1];
     }
   }
   r1[tid] = s1;
@@ -141,11 +141,11 @@ bn_bwd_finalize_kernel(const float *part, int R, int C, int Cs, double count,
   }
 }
 
-int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, double count,
+int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, int W, double count,
                            BNCoef coef, float *dgamma, float *dbeta, int training,
                            int accumulate, hipStream_t s) {
   HCU_TIMED(s, "bn_bwd_finalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, part, R, C,
-                     Cs, count, coef, dgamma, dbeta, training, accumulate));
+                     W, count, coef, dgamma, dbeta, training, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -304,6 +304,10 @@ int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef, int64_t n
 
 // Max-pool backward (argmax recomputed from y, first maximum in x,y,z window
 // order as torch's CPU max_pool3d) fused with the BatchNorm+ReLU reduction.
+// One thread per (pool window, channel quad): the window's y values are read
+// once, and dz is written for the window's voxels plus, for windows on the
+// last row/column/plane, the floor-mode remainder (which gets 0), so every
+// voxel of y is written exactly once and y is read from HBM once.
 __global__ void __launch_bounds__(256)
 bn_bwd_reduce_pool_kernel(const float *dP, const float *y, BNCoef coef, float *dz,
                           int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
@@ -319,60 +323,71 @@ bn_bwd_reduce_pool_kernel(const float *dP, const float *y, BNCoef coef, float *d
     const float4 sc = ld4(coef.scale + c), sh = ld4(coef.shift + c);
     const float4 mu = ld4(coef.mean + c), is = ld4(coef.invstd + c);
     for (int64_t e = beg + tid; e < end; e += g.tb) {
-      int64_t vox = e / C4;
-      const size_t off = (size_t)vox * Cs + c;
-      const int z = (int)(vox % Z);
-      vox /= Z;
-      const int yy = (int)(vox % Y);
-      vox /= Y;
-      const int x = (int)(vox % X);
-      const int b = (int)(vox / X);
-      const float4 yv = ld4(y + off);
-      const float4 zv = make_float4(fmaf(yv.x, sc.x, sh.x), fmaf(yv.y, sc.y, sh.y),
-                                    fmaf(yv.z, sc.z, sh.z), fmaf(yv.w, sc.w, sh.w));
-      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int wx = x / kx, wy = yy / ky, wz = z / kz;
-      if (wx < PX && wy < PY && wz < PZ) {
-        float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-        int4 am = make_int4(-1, -1, -1, -1);
-        int idx = 0;
-        for (int i = 0; i < kx; ++i)
-          for (int j = 0; j < ky; ++j)
-            for (int k = 0; k < kz; ++k, ++idx) {
-              const float4 t = ld4(
-                  y + ((((size_t)b * X + wx * kx + i) * Y + wy * ky + j) * Z + wz * kz + k) * Cs + c);
-              const float a0 = bnrelu(t.x, sc.x, sh.x), a1 = bnrelu(t.y, sc.y, sh.y);
-              const float a2 = bnrelu(t.z, sc.z, sh.z), a3 = bnrelu(t.w, sc.w, sh.w);
-              if (a0 > m.x) { m.x = a0; am.x = idx; }
-              if (a1 > m.y) { m.y = a1; am.y = idx; }
-              if (a2 > m.z) { m.z = a2; am.z = idx; }
-              if (a3 > m.w) { m.w = a3; am.w = idx; }
+      int64_t w = e / C4;
+      const int wz = (int)(w % PZ);
+      w /= PZ;
+      const int wy = (int)(w % PY);
+      w /= PY;
+      const int wx = (int)(w % PX);
+      const int b = (int)(w / PX);
+      const int x0 = wx * kx, y0 = wy * ky, z0 = wz * kz;
+      const int x1 = wx == PX - 1 ? X : x0 + kx, y1 = wy == PY - 1 ? Y : y0 + ky,
+                z1 = wz == PZ - 1 ? Z : z0 + kz;
+      // argmax of relu(bn(y)) over the window, first maximum wins
+      float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      int4 am = make_int4(-1, -1, -1, -1);
+      int idx = 0;
+      for (int i = 0; i < kx; ++i)
+        for (int j = 0; j < ky; ++j)
+          for (int k = 0; k < kz; ++k, ++idx) {
+            const float4 t = ld4(y + ((((size_t)b * X + x0 + i) * Y + y0 + j) * Z + z0 + k) * Cs + c);
+            const float a0 = bnrelu(t.x, sc.x, sh.x), a1 = bnrelu(t.y, sc.y, sh.y);
+            const float a2 = bnrelu(t.z, sc.z, sh.z), a3 = bnrelu(t.w, sc.w, sh.w);
+            if (a0 > m.x) { m.x = a0; am.x = idx; }
+            if (a1 > m.y) { m.y = a1; am.y = idx; }
+            if (a2 > m.z) { m.z = a2; am.z = idx; }
+            if (a3 > m.w) { m.w = a3; am.w = idx; }
+          }
+      const float4 gp = ld4(dP + ((((size_t)b * PX + wx) * PY + wy) * PZ + wz) * Cs + c);
+      for (int x = x0; x < x1; ++x)
+        for (int yy = y0; yy < y1; ++yy)
+          for (int z = z0; z < z1; ++z) {
+            const size_t off = ((((size_t)b * X + x) * Y + yy) * Z + z) * Cs + c;
+            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+            const bool inwin = x < x0 + kx && yy < y0 + ky && z < z0 + kz;
+            if (inwin) {
+              const int own = ((x - x0) * ky + (yy - y0)) * kz + (z - z0);
+              const float4 yv = ld4(y + off);   // L1/L2 hit: read just above
+              const float4 zv = make_float4(fmaf(yv.x, sc.x, sh.x), fmaf(yv.y, sc.y, sh.y),
+                                            fmaf(yv.z, sc.z, sh.z), fmaf(yv.w, sc.w, sh.w));
+              d.x = (am.x == own && zv.x > 0.f) ? gp.x : 0.f;
+              d.y = (am.y == own && zv.y > 0.f) ? gp.y : 0.f;
+              d.z = (am.z == own && zv.z > 0.f) ? gp.z : 0.f;
+              d.w = (am.w == own && zv.w > 0.f) ? gp.w : 0.f;
+              v[0] += d.x;
+              v[1] = fmaf(d.x, (yv.x - mu.x) * is.x, v[1]);
+              v[2] += d.y;
+              v[3] = fmaf(d.y, (yv.y - mu.y) * is.y, v[3]);
+              v[4] += d.z;
+              v[5] = fmaf(d.z, (yv.z - mu.z) * is.z, v[5]);
+              v[6] += d.w;
+              v[7] = fmaf(d.w, (yv.w - mu.w) * is.w, v[7]);
             }
-        const int own = ((x - wx * kx) * ky + (yy - wy * ky)) * kz + (z - wz * kz);
-        const float4 gp = ld4(dP + ((((size_t)b * PX + wx) * PY + wy) * PZ + wz) * Cs + c);
-        d.x = (am.x == own && zv.x > 0.f) ? gp.x : 0.f;
-        d.y = (am.y == own && zv.y > 0.f) ? gp.y : 0.f;
-        d.z = (am.z == own && zv.z > 0.f) ? gp.z : 0.f;
-        d.w = (am.w == own && zv.w > 0.f) ? gp.w : 0.f;
-      }
-      st4(dz + off, d);
-      v[0] += d.x;
-      v[1] = fmaf(d.x, (yv.x - mu.x) * is.x, v[1]);
-      v[2] += d.y;
-      v[3] = fmaf(d.y, (yv.y - mu.y) * is.y, v[3]);
-      v[4] += d.z;
-      v[5] = fmaf(d.z, (yv.z - mu.z) * is.z, v[5]);
-      v[6] += d.w;
-      v[7] = fmaf(d.w, (yv.w - mu.w) * is.w, v[7]);
+            st4(dz + off, d);
+          }
     }
   }
   block_reduce_c4<8>(v, lds, g.tb, C4, part + (size_t)blockIdx.x * Cs * 2);
 }
 
+int pool_bwd_rows(int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz) {
+  return bwd_rows((int64_t)B * (X / kx) * (Y / ky) * (Z / kz), Cs);
+}
+
 int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, float *dz,
                               int B, int X, int Y, int Z, int Cs, int kx, int ky,
                               int kz, float *part, int R, hipStream_t s) {
-  const RedGeom g = red_geom((int64_t)B * X * Y * Z, Cs, R);
+  const RedGeom g = red_geom((int64_t)B * (X / kx) * (Y / ky) * (Z / kz), Cs, R);
   HCU_TIMED(s, "bn_bwd_reduce_pool_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
                      (size_t)std::max(g.tb, 256) * 8 * 4, s, dP, y, coef, dz, B, X, Y, Z,
                      Cs, kx, ky, kz, part, g));

@@ -274,6 +274,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     if (int e = plan_conv_any(a, kTargetBlocks)) return e;
     u.dgrad = a;
     max_wprep = std::max(max_wprep, wprep_floats(a));
+    max_part = std::max(max_part, (size_t)gconv_rows(a) * a.CoutW * 2);
     max_kpart = std::max(max_kpart, conv_partial_floats(a));
   }
   {  // wgrad: rows = ci, cols = (t, co)
@@ -329,6 +330,7 @@ void track_conv(hcu_unet_plan &p, const ConvLayer &L) {
   p.max_act = std::max(p.max_act, std::max(L.in.floats(), L.out.floats()));
   p.max_part = std::max(p.max_part, (size_t)gconv_rows(L.fwd) * L.fwd.CoutW * 2);
   p.max_part = std::max(p.max_part, wgrad_partial_floats(L.wg));
+  p.max_part = std::max(p.max_part, (size_t)gconv_rows(L.dgrad) * L.dgrad.CoutW * 2);
   p.max_part = std::max(p.max_part, (size_t)bwd_rows(L.out.vox(), L.out.Cs) * L.out.Cs * 2);
   p.max_wprep = std::max(p.max_wprep, std::max(prep_floats_fwd(L), prep_floats_dgrad(L)));
   p.max_kpart = std::max(p.max_kpart, std::max(conv_partial_floats(L.fwd), conv_partial_floats(L.dgrad)));
@@ -570,9 +572,38 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
                                 c.p.spec.bn_momentum, training, coef, c.s);
 }
 
+// Sets up the dgrad epilogue that also performs the BatchNorm+ReLU backward
+// reduction of layer `bnl` (whose output the gradient is for); false when the
+// planned kernel cannot.
+bool fuse_bnbwd(const Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
+  if (!bnl || !conv_bnbwd_fusable(a)) return false;
+  const BNCoef coef = coef_at(c.sv, bnl->bn);
+  a.bn_y = c.fptr(c.sv, bnl->y_off);
+  a.bn_scale = coef.scale;
+  a.bn_shift = coef.shift;
+  a.bn_mean = coef.mean;
+  a.bn_invstd = coef.invstd;
+  a.stats = c.part();
+  return true;
+}
+
+// Finalize + apply of a BatchNorm backward whose reduction ran in a dgrad epilogue.
+int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *dz, int training,
+                 int accumulate) {
+  const BNCoef coef = coef_at(c.sv, bnl.bn);
+  if (int e = launch_bn_bwd_finalize(c.part(), gconv_rows(a), bnl.bn.C, bnl.bn.Cs, a.CoutW,
+                                     bnl.bn.count, coef, c.G + bnl.bn.gamma, c.G + bnl.bn.beta,
+                                     training, accumulate, c.s))
+    return e;
+  return launch_bn_bwd_apply(dz, c.fptr(c.sv, bnl.y_off), coef, bnl.out.vox(), bnl.out.Cs, c.s);
+}
+
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
+// With `bnl`, the input gradient leaves as d(pre-BN y) of layer bnl (its
+// BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
 int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float *asc,
-                  const float *ash, const float *dy, float *dA, int accumulate) {
+                  const float *ash, const float *dy, float *dA, int accumulate,
+                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
   tag(L.name, "wgrad");
   WGradArgs w = L.wg;
   w.A = A;
@@ -604,7 +635,13 @@ int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float 
   a.w = c.fptr(c.sv, L.wd_off);
   a.out = dA;
   a.partial = c.kpart();
-  return launch_conv_any(a, c.s);
+  const bool fused = fuse_bnbwd(c, a, bnl);
+  if (int e = launch_conv_any(a, c.s)) return e;
+  if (!fused) return 0;
+  tag(bnl->name, "bnbwd");
+  if (int e = finish_bnbwd(c, a, *bnl, dA, training, accumulate)) return e;
+  if (bn_done) *bn_done = true;
+  return 0;
 }
 
 // BatchNorm+ReLU backward for layer L: dbuf holds d(post-activation) on entry
@@ -626,7 +663,7 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
     if (int e = launch_bn_bwd_reduce_dense(dbuf, y, coef, nvox, L.out.Cs, c.part(), R, c.s))
       return e;
   }
-  if (int e = launch_bn_bwd_finalize(c.part(), R, L.bn.C, L.bn.Cs, L.bn.count, coef,
+  if (int e = launch_bn_bwd_finalize(c.part(), R, L.bn.C, L.bn.Cs, L.bn.Cs, L.bn.count, coef,
                                      c.G + L.bn.gamma, c.G + L.bn.beta, training, accumulate, c.s))
     return e;
   return launch_bn_bwd_apply(dbuf, y, coef, nvox, L.out.Cs, c.s);
@@ -792,7 +829,7 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
     if (int e = launch_outconv_wfinalize(part_oc, R, p.Co, last.out.C, last.out.Cs, c.G + p.oc_w,
                                          c.G + p.oc_b, accumulate, c.s))
       return e;
-    if (int e = launch_bn_bwd_finalize(part_bn, R, last.bn.C, last.bn.Cs, last.bn.count, coef,
+    if (int e = launch_bn_bwd_finalize(part_bn, R, last.bn.C, last.bn.Cs, last.bn.Cs, last.bn.count, coef,
                                        c.G + last.bn.gamma, c.G + last.bn.beta, training,
                                        accumulate, c.s))
       return e;
@@ -807,10 +844,13 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
     const BNCoef b1 = coef_at(c.sv, c1.bn);
     const float *U = c.fptr(c.sv, u.u_off);
     float *A = c.buf(cur), *Bf = c.buf(1 - cur);
-    // conv2
-    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate))
+    // conv2 (+ BatchNorm/ReLU backward of conv1, fused into its dgrad when possible)
+    bool done1 = false;
+    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate,
+                              &c1, training, &done1))
       return e;
-    if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
+    if (!done1)
+      if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
     // conv1 (folded cat)
     if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, A, accumulate)) return e;
     // up_conv: bias, weight, input gradients (A holds dU)
@@ -853,9 +893,15 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
       a.w = c.fptr(c.sv, u.wd_off);
       a.out = Bf;
       a.partial = c.kpart();
+      const bool fused = fuse_bnbwd(c, a, &prev);
       if (int e = launch_conv_any(a, c.s)) return e;
+      if (fused) {
+        tag(prev.name, "bnbwd");
+        if (int e = finish_bnbwd(c, a, prev, Bf, training, accumulate)) return e;
+      } else if (int e = bn_backward(c, prev, Bf, nullptr, nullptr, training, accumulate)) {
+        return e;
+      }
     }
-    if (int e = bn_backward(c, prev, Bf, nullptr, nullptr, training, accumulate)) return e;
     cur = 1 - cur;
   }
   // encoder, bottleneck to first
@@ -863,9 +909,12 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
     const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
     const BNCoef b1 = coef_at(c.sv, c1.bn);
     float *A = c.buf(cur), *Bf = c.buf(1 - cur);
-    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate))
+    bool done1 = false;
+    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate,
+                              &c1, training, &done1))
       return e;
-    if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
+    if (!done1)
+      if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
     const float *in = i == 0 ? c.fptr(c.sv, p.xcl_off) : c.fptr(c.sv, p.pool_off[i - 1]);
     float *dIn = (i > 0 || dx) ? A : nullptr;
     if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, dIn, accumulate)) return e;
