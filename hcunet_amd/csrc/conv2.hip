@@ -30,6 +30,7 @@
 #include "common.h"
 #include "timing.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 namespace hcu {
@@ -631,8 +632,15 @@ static int env_int(const char *name, int dflt) {
 }
 
 int plan_conv2(GConvArgs &a, int target_blocks) {
-  static const int mpw_target = env_int("HCU_CONV2_MPW_TARGET", 256);
-  static const int ks_target = env_int("HCU_CONV2_KS_TARGET", 256);
+  // debug: HCU_CONV2_SEL=k keeps the MPW target only for the k-th plan since
+  // the variable last changed (A/B bisection of one layer's tiling)
+  static int ncall = 0, last_sel = -1;
+  const int sel = env_int("HCU_CONV2_SEL", -1);
+  if (sel != last_sel) { ncall = 0; last_sel = sel; }
+  const int call = ncall++;
+  int mpw_target = env_int("HCU_CONV2_MPW_TARGET", 256);
+  const int ks_target = env_int("HCU_CONV2_KS_TARGET", 256);
+  if (sel >= 0 && sel != call) mpw_target = 1024;
   if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return fail(2, "conv2: empty output grid");
   if (a.ICs % 4 != 0 || a.OCs % 4 != 0) return fail(1, "conv2: channel strides must be multiples of 4");
   if (a.nph < 1) a.nph = 1;
@@ -647,9 +655,12 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
   const int ntz = cdiv(a.OZ, 16);
   a.TZ = cdiv(a.OZ, ntz);
   const int nN = a.CoutW / NT;
-  // MPW: largest tile that still gives enough tiles to fill the chip
+  // MPW: largest tile that still gives enough tiles to fill the chip and whose
+  // halo + epilogue images fit the LDS budget with some channel chunk CK
   const int mpws[3] = {4, 2, 1};
-  for (int mi = 0; mi < 3; ++mi) {
+  bool enough = false;
+  a.CK = 0;
+  for (int mi = 0; mi < 3 && !(enough && a.CK); ++mi) {
     const int MPW = mpws[mi];
     int TX, TY;
     tile2(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
@@ -657,26 +668,26 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
     a.MPW = MPW;
     a.TX = TX;
     a.TY = TY;
-    if (blocks >= (mpw_target ? mpw_target : target_blocks)) break;
+    a.HX = (a.TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
+    a.HY = (a.TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
+    a.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
+    enough = blocks >= (mpw_target ? mpw_target : target_blocks);
+    a.CK = 0;
+    const int cks[3] = {16, 8, 4};
+    for (int i = 0; i < 3; ++i) {
+      const int CK = cks[i];
+      if (a.ICs % CK) continue;
+      const long lds = conv2_lds(a, CK, NT);
+      if (lds <= 56 * 1024) {
+        a.CK = CK;
+        a.lds_bytes = (int)lds;
+        break;
+      }
+    }
   }
   a.ntx = cdiv(a.OX, a.TX);
   a.nty = cdiv(a.OY, a.TY);
   a.ntz = ntz;
-  a.HX = (a.TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
-  a.HY = (a.TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
-  a.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
-  a.CK = 0;
-  const int cks[3] = {16, 8, 4};
-  for (int i = 0; i < 3; ++i) {
-    const int CK = cks[i];
-    if (a.ICs % CK) continue;
-    const long lds = conv2_lds(a, CK, NT);
-    if (lds <= 56 * 1024) {
-      a.CK = CK;
-      a.lds_bytes = (int)lds;
-      break;
-    }
-  }
   if (!a.CK) return fail(4, "conv2: no tile fits in LDS");
   if (a.lds_bytes < 4 * NT * 2 * 4) a.lds_bytes = 4 * NT * 2 * 4;
   const long tiles = (long)a.ntx * a.nty * a.ntz * a.B;
@@ -715,6 +726,13 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
     a.epi_lds = 1;
   a.areg = (int)conv2_areg(a, a.CK, NT);
   a.use_conv2 = 1;
+  if (env_int("HCU_CONV2_LOG", 0))
+    fprintf(stderr,
+            "conv2 plan %d: B%d I%dx%dx%d ICs%d O%dx%dx%d S%dx%dx%d OCs%d Cout%d K%dx%dx%d s%d%d%d nph%d"
+            " | CK%d NSUB%d MPW%d T%dx%dx%d ks%d cps%d NPF%d gridx%d epi%d\n",
+            call, a.B, a.IX, a.IY, a.IZ, a.ICs, a.OX, a.OY, a.OZ, a.SX, a.SY, a.SZ, a.OCs, a.Cout,
+            a.KX, a.KY, a.KZ, a.sx, a.sy, a.sz, a.nph, a.CK, a.NSUB, a.MPW, a.TX, a.TY, a.TZ,
+            a.ksplit, a.cps, a.NPF, a.gridx, a.epi_lds);
   return 0;
 }
 

@@ -21,7 +21,9 @@
 #include "timing.h"
 #include "../../include/hcunet.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -319,6 +321,24 @@ struct hcu_unet_plan {
   size_t buf_off[2] = {0, 0};
   size_t part_off = 0, wprep_off = 0, kpart_off = 0;
   size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
+  // Captured launch sequences (hipGraph) keyed by the buffers they bake in:
+  // forward and backward are fixed kernel sequences, so a replay costs one
+  // launch on the host instead of one per kernel.
+  struct Graph {
+    std::vector<uintptr_t> key;
+    hipGraphExec_t exec = nullptr;
+    uint64_t used = 0;
+  };
+  mutable std::mutex gmu;
+  mutable std::vector<Graph> graphs;
+  mutable hipStream_t cap_stream = nullptr;
+  mutable int cap_device = -1;
+  mutable uint64_t gclock = 0;
+  ~hcu_unet_plan() {
+    for (Graph &g : graphs)
+      if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
+  }
 };
 
 namespace {
@@ -576,7 +596,8 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
 // reduction of layer `bnl` (whose output the gradient is for); false when the
 // planned kernel cannot.
 bool fuse_bnbwd(const Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
-  if (!bnl || !conv_bnbwd_fusable(a)) return false;
+  static const bool off = getenv("HCU_NO_BNFUSE") != nullptr;   // A/B debugging
+  if (off || !bnl || !conv_bnbwd_fusable(a)) return false;
   const BNCoef coef = coef_at(c.sv, bnl->bn);
   a.bn_y = c.fptr(c.sv, bnl->y_off);
   a.bn_scale = coef.scale;
@@ -671,6 +692,74 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
 
 }  // namespace
 
+namespace {
+
+bool graphs_enabled() {   // HCU_GRAPHS=0 launches kernel by kernel (debugging, A/B)
+  static const bool on = [] {
+    const char *e = getenv("HCU_GRAPHS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+void append_bn_key(std::vector<uintptr_t> &key, const hcu_unet_plan &p, const hcu_unet_tensors *t) {
+  for (int i = 0; i < p.n_bn; ++i) {
+    key.push_back(t->bn_running_mean ? (uintptr_t)t->bn_running_mean[i] : 0);
+    key.push_back(t->bn_running_var ? (uintptr_t)t->bn_running_var[i] : 0);
+    key.push_back(t->bn_num_batches_tracked ? (uintptr_t)t->bn_num_batches_tracked[i] : 0);
+  }
+}
+
+// Replays the captured launch sequence for `key`, capturing it on first use
+// (on a private stream, so nothing runs during capture) and keeping the 8
+// most recently used sequences.  Falls back to direct launches when graphs
+// are off or per-launch timing is on.
+template <class F>
+int run_graphed(const hcu_unet_plan &p, std::vector<uintptr_t> key, hipStream_t s, F enqueue) {
+  if (!graphs_enabled() || timing_on()) return enqueue(s);
+  int dev = 0;
+  HCU_HIP(hipGetDevice(&dev));
+  key.push_back((uintptr_t)dev);
+  std::lock_guard<std::mutex> lk(p.gmu);
+  for (auto &g : p.graphs)
+    if (g.key == key) {
+      g.used = ++p.gclock;
+      HCU_HIP(hipGraphLaunch(g.exec, s));
+      return HCU_OK;
+    }
+  if (!p.cap_stream || p.cap_device != dev) {
+    if (p.cap_stream) (void)hipStreamDestroy(p.cap_stream);
+    p.cap_stream = nullptr;
+    HCU_HIP(hipStreamCreateWithFlags(&p.cap_stream, hipStreamNonBlocking));
+    p.cap_device = dev;
+  }
+  HCU_HIP(hipStreamBeginCapture(p.cap_stream, hipStreamCaptureModeThreadLocal));
+  const int e = enqueue(p.cap_stream);
+  hipGraph_t graph = nullptr;
+  const hipError_t ce = hipStreamEndCapture(p.cap_stream, &graph);
+  if (e || ce != hipSuccess) {
+    if (graph) (void)hipGraphDestroy(graph);
+    if (e) return e;
+    return fail(HCU_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
+  }
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ie != hipSuccess)
+    return fail(HCU_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ie));
+  if (p.graphs.size() >= 8) {
+    auto lru = std::min_element(p.graphs.begin(), p.graphs.end(),
+                                [](const auto &a, const auto &b) { return a.used < b.used; });
+    (void)hipGraphExecDestroy(lru->exec);
+    p.graphs.erase(lru);
+  }
+  p.graphs.push_back({key, exec, ++p.gclock});
+  HCU_HIP(hipGraphLaunch(exec, s));
+  return HCU_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char *hcu_last_error(void) { return g_err.c_str(); }
@@ -714,17 +803,8 @@ int hcu_unet_plan_query(const hcu_unet_plan *p, int64_t *out_shape, int64_t *n_p
   return HCU_OK;
 }
 
-int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
-                     hcu_stream_t stream) {
-  if (!plan || !t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
-    return fail(HCU_ERR_INVALID, "null argument");
-  const hcu_unet_plan &p = *plan;
-  if (training) {
-    for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
-      for (const ConvLayer &L : *v)
-        if (L.bn.count <= 1.0)
-          return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
-  }
+static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,
+                           hipStream_t stream) {
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
@@ -804,11 +884,26 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   return HCU_OK;
 }
 
-int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, const float *dout,
-                      float *dx, int training, int accumulate, hcu_stream_t stream) {
-  if (!plan || !t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)
+int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
+                     hcu_stream_t stream) {
+  if (!plan || !t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
     return fail(HCU_ERR_INVALID, "null argument");
   const hcu_unet_plan &p = *plan;
+  if (training) {
+    for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
+      for (const ConvLayer &L : *v)
+        if (L.bn.count <= 1.0)
+          return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
+  }
+  std::vector<uintptr_t> key = {0, (uintptr_t)t->x, (uintptr_t)t->out, (uintptr_t)t->params,
+                                (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)training};
+  append_bn_key(key, p, t);
+  return run_graphed(p, key, (hipStream_t)stream,
+                     [&](hipStream_t s) { return enqueue_forward(p, t, training, s); });
+}
+
+static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout,
+                            float *dx, int training, int accumulate, hipStream_t stream) {
   const hcu_unet_spec &s = p.spec;
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   int cur = 0;  // index of the buffer holding the current d(pre-BN y)
@@ -928,6 +1023,20 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
   }
   if (timing_on()) timing_set_tag("");
   return HCU_OK;
+}
+
+
+int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, const float *dout,
+                      float *dx, int training, int accumulate, hcu_stream_t stream) {
+  if (!plan || !t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)
+    return fail(HCU_ERR_INVALID, "null argument");
+  const hcu_unet_plan &p = *plan;
+  std::vector<uintptr_t> key = {1, (uintptr_t)t->x, (uintptr_t)t->params, (uintptr_t)t->grads,
+                                (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)dout,
+                                (uintptr_t)dx, (uintptr_t)training, (uintptr_t)accumulate};
+  return run_graphed(p, key, (hipStream_t)stream, [&](hipStream_t s) {
+    return enqueue_backward(p, t, dout, dx, training, accumulate, s);
+  });
 }
 
 }  // extern "C"

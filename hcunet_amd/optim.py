@@ -8,6 +8,8 @@ whole group is updated by a single hcu_adam_step launch; otherwise each
 tensor gets its own launch.  Optimizer state keeps torch's per-parameter
 layout ('step', 'exp_avg', 'exp_avg_sq'), so state_dict() is compatible.
 """
+import ctypes
+
 import torch
 
 from . import _lib
@@ -55,10 +57,11 @@ class Adam(torch.optim.Optimizer):
             n = sum(p.numel() for p in ps)
             M = torch.zeros(n, dtype=torch.float32, device=dev)
             V = torch.zeros(n, dtype=torch.float32, device=dev)
+            step = torch.tensor(0.0)   # one step counter shared by the flat group
             off = 0
             for p, s in zip(ps, states):
                 k = p.numel()
-                s['step'] = torch.tensor(0.0)
+                s['step'] = step
                 s['exp_avg'] = M[off:off + k].view_as(p)
                 s['exp_avg_sq'] = V[off:off + k].view_as(p)
                 off += k
@@ -69,6 +72,37 @@ class Adam(torch.optim.Optimizer):
                     s['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     s['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
 
+    def _fast_step(self, L, gi, group):
+        """One launch for a group whose flat layout was verified on a previous
+        step: re-checked with O(1) pointer tests instead of a pass over every
+        parameter (the per-step host cost of the optimizer)."""
+        fast = getattr(self, '_fast', None)
+        if fast is None:
+            self._fast = fast = {}
+        f = fast.get(gi)
+        if f is None:
+            return False
+        plist, n_list, p0, pl, pbase, gbase, n, M, V, step_t = f
+        g0, gl = p0.grad, pl.grad
+        if (group['params'] is not plist or len(plist) != n_list or g0 is None or gl is None
+                or p0.data_ptr() != pbase or g0.data_ptr() != gbase
+                or gl.data_ptr() != gbase + 4 * (n - pl.numel())
+                or pl.data_ptr() != pbase + 4 * (n - pl.numel())):
+            fast.pop(gi, None)
+            return False
+        # every parameter in between must also have a gradient (same flat buffer)
+        if any(p.grad is None for p in plist):
+            fast.pop(gi, None)
+            return False
+        step = int(step_t.item()) + 1
+        step_t.fill_(step)
+        b1, b2 = group['betas']
+        _lib.check(L.hcu_adam_step(
+            ctypes.c_void_p(pbase), ctypes.c_void_p(gbase), _lib.ptr(M), _lib.ptr(V), n,
+            group['lr'], b1, b2, group['eps'], group['weight_decay'], step, 1.0,
+            _lib.stream_handle(p0.device)), 'Adam.step')
+        return True
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -76,7 +110,9 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         L = _lib.lib()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
+            if self._fast_step(L, gi, group):
+                continue
             ps = [p for p in group['params'] if p.grad is not None]
             if not ps:
                 continue
@@ -98,12 +134,17 @@ class Adam(torch.optim.Optimizer):
             stream = _lib.stream_handle(ps[0].device)
             if flat:
                 step = int(float(states[0]['step'])) + 1
-                for s in states:
+                shared = all(s['step'] is states[0]['step'] for s in states)
+                for s in (states[:1] if shared else states):
                     s['step'].fill_(step)
                 _lib.check(L.hcu_adam_step(
                     _lib.ptr(prun[0]), _lib.ptr(grun[0]), _lib.ptr(mrun[0]), _lib.ptr(vrun[0]),
                     prun[1], group['lr'], b1, b2, group['eps'], group['weight_decay'], step, 1.0,
                     stream), 'Adam.step')
+                if shared:
+                    self._fast[gi] = (group['params'], len(group['params']), ps[0], ps[-1],
+                                      prun[0].data_ptr(), grun[0].data_ptr(), prun[1],
+                                      mrun[0], vrun[0], states[0]['step'])
             else:
                 for p, s in zip(ps, states):
                     g = p.grad

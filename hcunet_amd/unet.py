@@ -19,6 +19,7 @@ single launches over contiguous memory.
 """
 import ctypes
 import glob
+import os
 
 import torch
 import torch.nn as nn
@@ -476,6 +477,9 @@ class _Engine:
         return tmp, 0, finish_mixed
 
 
+_POISON = os.environ.get('HCU_POISON') == '1'
+
+
 class _UnetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, eng, *params):
@@ -485,6 +489,9 @@ class _UnetFunction(torch.autograd.Function):
         out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
         saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
+        if _POISON:   # debugging: every byte the step does not write reads as NaN
+            saved.fill_(255)
+            scratch.fill_(255)
         training = 1 if eng.module_ref.training else 0
         t = eng.tensors(x, out, saved, scratch)
         _lib.check(_lib.lib().hcu_unet_forward(plan.handle, ctypes.byref(t), training,
@@ -505,6 +512,8 @@ class _UnetFunction(torch.autograd.Function):
         if dout.dtype != torch.float32:
             dout = dout.float()
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
+        if _POISON:
+            scratch.fill_(255)
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         G, accumulate, finish = eng.grad_target()
         t = eng.tensors(x, None, saved, scratch, grads=G)
