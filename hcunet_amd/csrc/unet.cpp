@@ -301,6 +301,8 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 
 }  // namespace
 
+#define HCU_NBUF 6
+
 struct hcu_unet_plan {
   hcu_unet_spec spec;
   int B, X, Y, Z, L;
@@ -318,8 +320,11 @@ struct hcu_unet_plan {
   std::vector<PrepJob> prep_jobs;  // weight re-layouts, one batched launch per forward
   size_t saved_bytes = 0, scratch_bytes = 0;
   // scratch layout
-  size_t buf_off[2] = {0, 0};
-  size_t part_off = 0, wprep_off = 0, kpart_off = 0;
+  // Backward gradient buffers: a ring of HCU_NBUF activation-sized slots, so
+  // a slot read by the weight-gradient branch is rewritten only several
+  // layers later (see Ctx::alloc).
+  size_t buf_off[HCU_NBUF] = {};
+  size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
   size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
   // Captured launch sequences (hipGraph) keyed by the buffers they bake in:
   // forward and backward are fixed kernel sequences, so a replay costs one
@@ -334,10 +339,27 @@ struct hcu_unet_plan {
   mutable hipStream_t cap_stream = nullptr;
   mutable int cap_device = -1;
   mutable uint64_t gclock = 0;
+  // Weight-gradient branch of the backward: its own stream and the events
+  // that order it against the data-gradient chain (created on first use).
+  mutable std::mutex smu;
+  mutable hipStream_t side = nullptr;
+  mutable int side_device = -1;
+  mutable hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_slot[HCU_NBUF] = {};
+  void destroy_side() const {
+    if (side) (void)hipStreamDestroy(side);
+    for (hipEvent_t *e : {&ev_fork, &ev_join})
+      if (*e) (void)hipEventDestroy(*e);
+    for (hipEvent_t &e : ev_slot)
+      if (e) (void)hipEventDestroy(e);
+    side = nullptr;
+    ev_fork = ev_join = nullptr;
+    for (hipEvent_t &e : ev_slot) e = nullptr;
+  }
   ~hcu_unet_plan() {
     for (Graph &g : graphs)
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    destroy_side();
   }
 };
 
@@ -543,9 +565,9 @@ int build_plan(hcu_unet_plan &p) {
   p.saved_bytes = saved.off;
 
   Region scratch;
-  p.buf_off[0] = scratch.take_floats(p.max_act);
-  p.buf_off[1] = scratch.take_floats(p.max_act);
+  for (size_t &b : p.buf_off) b = scratch.take_floats(p.max_act);
   p.part_off = scratch.take_floats(p.max_part);
+  p.wpart_off = scratch.take_floats(p.max_part);
   p.wprep_off = scratch.take_floats(p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
   p.scratch_bytes = scratch.off;
@@ -559,11 +581,48 @@ struct Ctx {
   char *sv, *sc;
   const float *P;
   float *G;
+  // Backward only: the weight-gradient branch runs on `ws` (== s when not
+  // split).  It reads gradient slots the main chain has finished and writes
+  // only its own partials (wpart) and the parameter gradients, so the one
+  // hazard is the main chain reusing a slot the branch has not read yet.
+  hipStream_t ws = nullptr;
+  bool split = false;
+  int next_slot = 0;
+  unsigned slot_read = 0;   // slots whose last reader event was recorded in this enqueue
   float *fptr(char *base, size_t off) const { return reinterpret_cast<float *>(base + off); }
   float *part() const { return fptr(sc, p.part_off); }
+  float *wpart() const { return fptr(sc, split ? p.wpart_off : p.part_off); }
   float *wprep() const { return fptr(sc, p.wprep_off); }
   float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
   float *kpart() const { return fptr(sc, p.kpart_off); }
+  hipStream_t wstream() const { return split ? ws : s; }
+  // Fresh slot for the main chain to write; waits for the branch's last read of it.
+  int alloc(int &slot) {
+    slot = next_slot;
+    next_slot = (next_slot + 1) % HCU_NBUF;
+    if (split && (slot_read & (1u << slot))) HCU_HIP(hipStreamWaitEvent(s, p.ev_slot[slot], 0));
+    return HCU_OK;
+  }
+  // Branch work issued from here on sees everything the main chain has issued.
+  int fork() {
+    if (!split) return HCU_OK;
+    HCU_HIP(hipEventRecord(p.ev_fork, s));
+    HCU_HIP(hipStreamWaitEvent(ws, p.ev_fork, 0));
+    return HCU_OK;
+  }
+  // The branch work issued so far is the last reader of `slot`.
+  int read_done(int slot) {
+    if (!split || slot < 0) return HCU_OK;
+    HCU_HIP(hipEventRecord(p.ev_slot[slot], ws));
+    slot_read |= 1u << slot;
+    return HCU_OK;
+  }
+  int join() {
+    if (!split) return HCU_OK;
+    HCU_HIP(hipEventRecord(p.ev_join, ws));
+    HCU_HIP(hipStreamWaitEvent(s, p.ev_join, 0));
+    return HCU_OK;
+  }
 };
 
 void tag(const std::string &layer, const char *phase) {
@@ -622,19 +681,20 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
 // With `bnl`, the input gradient leaves as d(pre-BN y) of layer bnl (its
 // BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
-int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float *asc,
-                  const float *ash, const float *dy, float *dA, int accumulate,
+int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
+                  const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
                   const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
   tag(L.name, "wgrad");
+  if (int e = c.fork()) return e;
   WGradArgs w = L.wg;
   w.A = A;
   w.a_scale = asc;
   w.a_shift = ash;
   w.G = dy;
-  w.partial = c.part();
-  if (int e = launch_wgrad(w, c.s)) return e;
+  w.partial = c.wpart();
+  if (int e = launch_wgrad(w, c.wstream())) return e;
   WGradFinalize f{};
-  f.partial = c.part();
+  f.partial = c.wpart();
   f.dw = c.G + L.w_off;
   f.db = c.G + L.b_off;
   f.KB = w.KB;
@@ -648,7 +708,8 @@ int conv_backward(const Ctx &c, const ConvLayer &L, const float *A, const float 
   f.fold_mod = L.fold_mod;
   f.ACs = w.ACs;
   f.accumulate = accumulate;
-  if (int e = launch_wgrad_finalize(f, c.s)) return e;
+  if (int e = launch_wgrad_finalize(f, c.wstream())) return e;
+  if (int e = c.read_done(dy_slot)) return e;
   if (!dA) return 0;
   tag(L.name, "dgrad");
   GConvArgs a = L.dgrad;
@@ -903,10 +964,14 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
 }
 
 static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout,
-                            float *dx, int training, int accumulate, hipStream_t stream) {
+                            float *dx, int training, int accumulate, hipStream_t stream,
+                            bool split) {
   const hcu_unet_spec &s = p.spec;
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
-  int cur = 0;  // index of the buffer holding the current d(pre-BN y)
+  c.split = split;
+  c.ws = split ? p.side : c.s;
+  int cur = 0;  // slot holding the current d(pre-BN y)
+  if (int e = c.alloc(cur)) return e;
 
   // out_conv + last BatchNorm
   const ConvLayer &last = p.uc2[p.L - 2];
@@ -938,36 +1003,42 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     const ConvTLayer &u = p.up[j];
     const BNCoef b1 = coef_at(c.sv, c1.bn);
     const float *U = c.fptr(c.sv, u.u_off);
-    float *A = c.buf(cur), *Bf = c.buf(1 - cur);
+    int sb = 0, su = 0, sd = 0;
     // conv2 (+ BatchNorm/ReLU backward of conv1, fused into its dgrad when possible)
+    if (int e = c.alloc(sb)) return e;
+    float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
-    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate,
-                              &c1, training, &done1))
+    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
+                              accumulate, &c1, training, &done1))
       return e;
     if (!done1)
       if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
-    // conv1 (folded cat)
-    if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, A, accumulate)) return e;
-    // up_conv: bias, weight, input gradients (A holds dU)
-    tag(u.name, "wgrad");
-    {
-      const int R = chansum_rows(u.out.vox(), u.out.Cs);
-      if (int e = launch_chansum(A, u.out.vox(), u.out.Cs, c.part(), R, c.s)) return e;
-      if (int e = launch_reduce_partials(c.part(), R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate, c.s))
-        return e;
-    }
+    // conv1 (folded cat): dU into a fresh slot
+    if (int e = c.alloc(su)) return e;
+    float *dU = c.buf(su);
+    if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, sb, dU, accumulate)) return e;
+    // up_conv: bias and weight gradients on the branch, input gradient on the chain
     const ConvLayer &prev = j == 0 ? p.dc2[p.L - 1] : p.uc2[j - 1];
     const BNCoef bp = coef_at(c.sv, prev.bn);
+    tag(u.name, "wgrad");
+    if (int e = c.fork()) return e;
+    {
+      const int R = chansum_rows(u.out.vox(), u.out.Cs);
+      if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, c.wpart(), R, c.wstream())) return e;
+      if (int e = launch_reduce_partials(c.wpart(), R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate,
+                                         c.wstream()))
+        return e;
+    }
     {
       WGradArgs w = u.wg;
       w.A = c.fptr(c.sv, prev.y_off);
       w.a_scale = bp.scale;
       w.a_shift = bp.shift;
-      w.G = A;
-      w.partial = c.part();
-      if (int e = launch_wgrad(w, c.s)) return e;
+      w.G = dU;
+      w.partial = c.wpart();
+      if (int e = launch_wgrad(w, c.wstream())) return e;
       WGradFinalize f{};
-      f.partial = c.part();
+      f.partial = c.wpart();
       f.dw = c.G + u.w_off;
       f.db = nullptr;
       f.KB = w.KB;
@@ -979,50 +1050,83 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       f.CoutT = u.Cout;
       f.GCs = w.GCs;
       f.accumulate = accumulate;
-      if (int e = launch_wgrad_finalize(f, c.s)) return e;
+      if (int e = launch_wgrad_finalize(f, c.wstream())) return e;
     }
+    if (int e = c.read_done(su)) return e;
     tag(u.name, "dgrad");
+    if (int e = c.alloc(sd)) return e;
     {
+      float *dP = c.buf(sd);
       GConvArgs a = u.dgrad;
-      a.in = A;
+      a.in = dU;
       a.w = c.fptr(c.sv, u.wd_off);
-      a.out = Bf;
+      a.out = dP;
       a.partial = c.kpart();
       const bool fused = fuse_bnbwd(c, a, &prev);
       if (int e = launch_conv_any(a, c.s)) return e;
       if (fused) {
         tag(prev.name, "bnbwd");
-        if (int e = finish_bnbwd(c, a, prev, Bf, training, accumulate)) return e;
-      } else if (int e = bn_backward(c, prev, Bf, nullptr, nullptr, training, accumulate)) {
+        if (int e = finish_bnbwd(c, a, prev, dP, training, accumulate)) return e;
+      } else if (int e = bn_backward(c, prev, dP, nullptr, nullptr, training, accumulate)) {
         return e;
       }
     }
-    cur = 1 - cur;
+    cur = sd;
   }
   // encoder, bottleneck to first
   for (int i = p.L - 1; i >= 0; --i) {
     const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
     const BNCoef b1 = coef_at(c.sv, c1.bn);
-    float *A = c.buf(cur), *Bf = c.buf(1 - cur);
+    int sb = 0, sa = -1;
+    if (int e = c.alloc(sb)) return e;
+    float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
-    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, Bf, accumulate,
-                              &c1, training, &done1))
+    if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
+                              accumulate, &c1, training, &done1))
       return e;
     if (!done1)
       if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
     const float *in = i == 0 ? c.fptr(c.sv, p.xcl_off) : c.fptr(c.sv, p.pool_off[i - 1]);
-    float *dIn = (i > 0 || dx) ? A : nullptr;
-    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, dIn, accumulate)) return e;
+    float *dIn = nullptr;
+    if (i > 0 || dx) {
+      if (int e = c.alloc(sa)) return e;
+      dIn = c.buf(sa);
+    }
+    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate)) return e;
     if (i > 0) {
-      // A = d(pooled), produce d(pre-BN y2_{i-1}) into Bf
-      if (int e = bn_backward(c, p.dc2[i - 1], Bf, A, s.pool_k, training, accumulate)) return e;
-      cur = 1 - cur;
+      // dIn = d(pooled): produce d(pre-BN y2_{i-1}) into a fresh slot
+      int sp = 0;
+      if (int e = c.alloc(sp)) return e;
+      if (int e = bn_backward(c, p.dc2[i - 1], c.buf(sp), dIn, s.pool_k, training, accumulate))
+        return e;
+      cur = sp;
     } else if (dx) {
-      if (int e = launch_from_cl(A, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
+      if (int e = launch_from_cl(dIn, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
     }
   }
+  if (int e = c.join()) return e;
   if (timing_on()) timing_set_tag("");
   return HCU_OK;
+}
+
+// Creates the weight-gradient branch's stream and events on `dev` (once).
+int ensure_side(const hcu_unet_plan &p, int dev) {
+  if (p.side && p.side_device == dev) return HCU_OK;
+  p.destroy_side();
+  HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+  p.side_device = dev;
+  for (hipEvent_t *e : {&p.ev_fork, &p.ev_join})
+    HCU_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t &e : p.ev_slot) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return HCU_OK;
+}
+
+bool side_enabled() {   // HCU_SIDE=0 keeps the whole backward on one stream (A/B, debugging)
+  static const bool on = [] {
+    const char *e = getenv("HCU_SIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 
@@ -1034,8 +1138,18 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
   std::vector<uintptr_t> key = {1, (uintptr_t)t->x, (uintptr_t)t->params, (uintptr_t)t->grads,
                                 (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)dout,
                                 (uintptr_t)dx, (uintptr_t)training, (uintptr_t)accumulate};
+  // Per-launch timing attributes kernel time to layers: keep it serial.
+  const bool split = side_enabled() && !timing_on();
+  std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
+  if (split) {
+    lk.lock();   // one user of the branch stream and its events at a time
+    int dev = 0;
+    HCU_HIP(hipGetDevice(&dev));
+    if (int e = ensure_side(p, dev)) return e;
+  }
+  key.push_back((uintptr_t)split);
   return run_graphed(p, key, (hipStream_t)stream, [&](hipStream_t s) {
-    return enqueue_backward(p, t, dout, dx, training, accumulate, s);
+    return enqueue_backward(p, t, dout, dx, training, accumulate, s, split);
   });
 }
 
