@@ -64,6 +64,15 @@ class ConvDesc(ctypes.Structure):
     ]
 
 
+class BNLayerInfo(ctypes.Structure):
+    _fields_ = [
+        ("y_offset", ctypes.c_int64), ("coef_offset", ctypes.c_int64),
+        ("B", ctypes.c_int), ("X", ctypes.c_int), ("Y", ctypes.c_int), ("Z", ctypes.c_int),
+        ("C", ctypes.c_int), ("Cs", ctypes.c_int), ("elem_bytes", ctypes.c_int),
+        ("pad", ctypes.c_int),
+    ]
+
+
 # Every symbol include/hcunet.h declares: (name, restype, argtypes)
 _VP, _I, _I64, _F, _SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
 SYMBOLS = [
@@ -73,6 +82,7 @@ SYMBOLS = [
     ("hcu_unet_plan_destroy", None, [_VP]),
     ("hcu_unet_plan_query", _I, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                                  ctypes.POINTER(_I), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
+    ("hcu_unet_plan_bn_layers", _I, [_VP, ctypes.POINTER(BNLayerInfo), _I]),
     ("hcu_unet_forward", _I, [_VP, ctypes.POINTER(UnetTensors), _I, _VP]),
     ("hcu_unet_backward", _I, [_VP, ctypes.POINTER(UnetTensors), _VP, _VP, _I, _I, _VP]),
     ("hcu_loss_pixel_scratch_bytes", _SZ, [_I64]),

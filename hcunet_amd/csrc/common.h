@@ -100,6 +100,13 @@ struct GConvArgs {
   const float *bn_y, *bn_scale, *bn_shift, *bn_mean, *bn_invstd;
   double flops;                       // algorithmic FLOPs (0: derive)
 };
+// Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
+// (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n
+// outputs the row's workgroup produced, K a pivot value taken from those
+// outputs.  bn_fwd_finalize combines the rows in fp64 (parallel-variance
+// identity), so the variance never comes from E[y^2] - E[y]^2 of raw fp32 sums.
+// The fused BatchNorm-backward epilogue (bn_y set) writes plain [rows][CoutW][2]
+// sums (sum dz, sum dz * xhat) into the same buffer.
 // Chooses the tile and kernel variant; returns 0 or an error code.
 int plan_gconv(GConvArgs &a, int target_blocks);
 int launch_gconv(const GConvArgs &a, hipStream_t s);

@@ -190,13 +190,20 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
 
   const bool split = a.ksplit > 1;
   float *dst = split ? a.partial + (size_t)blockIdx.z * a.slice_floats : a.out;
+  // Forward statistics are taken about a block-wide pivot per channel (the
+  // value of the block's first output voxel; StatRow in common.h); the fused
+  // BatchNorm-backward sums (bn_y set) are plain sums.
+  const bool fwdstat = a.stats && !a.bn_y && !split;
+  float *pivl = reinterpret_cast<float *>(rowoff + MPW * 64);   // [NT] pivot broadcast
+  float pv[NSUB], cnt = 0.f;
+  bool have_piv = false;
   // per-column store offset relative to the voxel (channel + output phase), or -1
   float s1[NSUB], s2[NSUB], bias_v[NSUB];
   int coff[NSUB];
   bool cst[NSUB];
 #pragma unroll
   for (int n = 0; n < NSUB; ++n) {
-    s1[n] = s2[n] = 0.f;
+    s1[n] = s2[n] = pv[n] = 0.f;
     const int nn = n0 + n * 16 + r16;
     bias_v[n] = (!split && a.bias && nn < a.Cout * a.nph) ? a.bias[nn % a.Cout] : 0.f;
     int off = -1, co = nn;
@@ -218,6 +225,16 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     float *tp = dst + ((((size_t)b * a.SX + ox0 * a.osx + a.ofx) * a.SY + oy0 * a.osy + a.ofy) *
                            a.SZ + oz0 * a.osz + a.ofz) * a.OCs;
     const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
+    if (fwdstat && !have_piv) {   // block-uniform: the first tile of this block
+      if (wave == 0 && g == 0) {
+#pragma unroll
+        for (int n = 0; n < NSUB; ++n) pivl[n * 16 + r16] = acc[0][n][0] + bias_v[n];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int n = 0; n < NSUB; ++n) pv[n] = pivl[n * 16 + r16];
+      have_piv = true;
+    }
 #pragma unroll
     for (int j = 0; j < MPW; ++j) {
       const int m = wave + 4 * j;
@@ -234,6 +251,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
           }
           if (ok) {
             float *vp = tp + ro;
+            cnt += 1.f;
 #pragma unroll
             for (int n = 0; n < NSUB; ++n) {
               if (coff[n] < 0) continue;
@@ -251,8 +269,9 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
               }
               vp[coff[n]] = val;
               if (cst[n]) {
-                s1[n] += val;
-                s2[n] = fmaf(val, val, s2[n]);
+                const float d = val - pv[n];
+                s1[n] += d;
+                s2[n] = fmaf(d, d, s2[n]);
               }
             }
             if (zpad) {   // ConvTranspose3d phases: zero the padded channels of U
@@ -284,7 +303,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     bias4.z = cc + 2 < a.Cout ? a.bias[cc + 2] : 0.f;
     bias4.w = cc + 3 < a.Cout ? a.bias[cc + 3] : 0.f;
   }
-  float4 st1 = make_float4(0.f, 0.f, 0.f, 0.f), st2 = st1;
+  float4 st1 = make_float4(0.f, 0.f, 0.f, 0.f), st2 = st1, piv4 = st1;
   float4 bsc = st1, bsh = st1, bmu = st1, bis = st1;
   if (a.bn_y && a.epi_lds) {
     const int cc = n0 + ec4 * 4;
@@ -311,6 +330,14 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
                            a.SZ + oz0 * a.osz + a.ofz) * a.OCs + n0 + ec4 * 4;
     const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
     const int vstep = 256 / nc4;
+    if (fwdstat && !have_piv) {   // pivot: the block's first output voxel (row 0, always valid)
+      piv4 = *reinterpret_cast<const float4 *>(smem + ec4 * 4);
+      piv4.x += bias4.x;
+      piv4.y += bias4.y;
+      piv4.z += bias4.z;
+      piv4.w += bias4.w;
+      have_piv = true;
+    }
     for (int i = tid / nc4; i < MT; i += vstep) {
       bool ok = true;
       if (!interior) {
@@ -338,11 +365,13 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
           continue;
         }
         *reinterpret_cast<float4 *>(tp + rowoff[i]) = v;
-        st1.x += v.x; st1.y += v.y; st1.z += v.z; st1.w += v.w;
-        st2.x = fmaf(v.x, v.x, st2.x);
-        st2.y = fmaf(v.y, v.y, st2.y);
-        st2.z = fmaf(v.z, v.z, st2.z);
-        st2.w = fmaf(v.w, v.w, st2.w);
+        const float4 d = make_float4(v.x - piv4.x, v.y - piv4.y, v.z - piv4.z, v.w - piv4.w);
+        st1.x += d.x; st1.y += d.y; st1.z += d.z; st1.w += d.w;
+        st2.x = fmaf(d.x, d.x, st2.x);
+        st2.y = fmaf(d.y, d.y, st2.y);
+        st2.z = fmaf(d.z, d.z, st2.z);
+        st2.w = fmaf(d.w, d.w, st2.w);
+        cnt += 1.f;
       }
     }
   };
@@ -460,22 +489,31 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   }
 
   if (a.stats && !split && a.epi_lds) {
-    // fixed-order combine of the threads that share a channel group
+    // fixed-order combine of the threads that share a channel group (they
+    // share the pivot too, so their pivoted sums add)
     __syncthreads();
-    float *red = smem;  // [256][8]
-    red[tid * 8 + 0] = st1.x; red[tid * 8 + 1] = st1.y; red[tid * 8 + 2] = st1.z; red[tid * 8 + 3] = st1.w;
-    red[tid * 8 + 4] = st2.x; red[tid * 8 + 5] = st2.y; red[tid * 8 + 6] = st2.z; red[tid * 8 + 7] = st2.w;
+    float *red = smem;  // [256][12]
+    red[tid * 12 + 0] = st1.x; red[tid * 12 + 1] = st1.y; red[tid * 12 + 2] = st1.z; red[tid * 12 + 3] = st1.w;
+    red[tid * 12 + 4] = st2.x; red[tid * 12 + 5] = st2.y; red[tid * 12 + 6] = st2.z; red[tid * 12 + 7] = st2.w;
+    red[tid * 12 + 8] = cnt;
     __syncthreads();
     if (tid < nc4 * 4) {
       const int c4 = tid >> 2, comp = tid & 3;
-      float t1 = 0.f, t2 = 0.f;
+      float t1 = 0.f, t2 = 0.f, tn = 0.f;
       for (int k = c4; k < 256; k += nc4) {
-        t1 += red[k * 8 + comp];
-        t2 += red[k * 8 + 4 + comp];
+        t1 += red[k * 12 + comp];
+        t2 += red[k * 12 + 4 + comp];
+        tn += red[k * 12 + 8];
       }
       const size_t row = blockIdx.x;
-      a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
-      a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+      if (fwdstat) {
+        const float pk = comp == 0 ? piv4.x : (comp == 1 ? piv4.y : (comp == 2 ? piv4.z : piv4.w));
+        *reinterpret_cast<float4 *>(a.stats + (row * a.CoutW + n0 + tid) * 4) =
+            make_float4(t1, t2, pk, tn);
+      } else {
+        a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
+        a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+      }
     }
   } else if (a.stats && !split) {
 #pragma unroll
@@ -485,26 +523,35 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
       s2[n] += __shfl_xor(s2[n], 16);
       s2[n] += __shfl_xor(s2[n], 32);
     }
+    cnt += __shfl_xor(cnt, 16);
+    cnt += __shfl_xor(cnt, 32);
     __syncthreads();
-    float *red = smem;  // [4][NT][2]
+    float *red = smem;  // [4][NT][3]
     if (lane < 16) {
 #pragma unroll
       for (int n = 0; n < NSUB; ++n) {
-        red[(wave * NT + n * 16 + lane) * 2 + 0] = s1[n];
-        red[(wave * NT + n * 16 + lane) * 2 + 1] = s2[n];
+        red[(wave * NT + n * 16 + lane) * 3 + 0] = s1[n];
+        red[(wave * NT + n * 16 + lane) * 3 + 1] = s2[n];
+        red[(wave * NT + n * 16 + lane) * 3 + 2] = cnt;
       }
     }
     __syncthreads();
     if (tid < NT) {
-      float t1 = 0.f, t2 = 0.f;
+      float t1 = 0.f, t2 = 0.f, tn = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        t1 += red[(w * NT + tid) * 2 + 0];
-        t2 += red[(w * NT + tid) * 2 + 1];
+        t1 += red[(w * NT + tid) * 3 + 0];
+        t2 += red[(w * NT + tid) * 3 + 1];
+        tn += red[(w * NT + tid) * 3 + 2];
       }
       const size_t row = blockIdx.x;
-      a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
-      a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+      if (fwdstat) {
+        *reinterpret_cast<float4 *>(a.stats + (row * a.CoutW + n0 + tid) * 4) =
+            make_float4(t1, t2, pivl[tid], tn);
+      } else {
+        a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
+        a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+      }
     }
   }
 }
@@ -515,7 +562,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
 // exactly one (voxel, channel) of the GEMM, so the slices are fully written.
 // Requires 256 % (OCs/4) == 0 (plan_conv2 only splits such layers).
 __global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, int vox_per_block) {
-  __shared__ float red[256][2];
+  __shared__ float red[256][3];
   const int64_t nvox = (int64_t)a.B * a.SX * a.SY * a.SZ;
   const int C4 = a.OCs / 4;
   const int tid = threadIdx.x;
@@ -532,7 +579,7 @@ __global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, in
     bv.w = c + 3 < a.Cout ? a.bias[c + 3] : 0.f;
   }
   float st1[4] = {0.f, 0.f, 0.f, 0.f}, st2[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int64_t v = v0 + tid / C4; v < v1; v += vstep) {
+  auto vsum = [&](int64_t v) {
     const size_t off = (size_t)v * a.OCs + c4 * 4;
     float4 s = *reinterpret_cast<const float4 *>(a.partial + off);
     for (int k = 1; k < a.ksplit; ++k) {
@@ -546,6 +593,16 @@ __global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, in
     s.y += bv.y;
     s.z += bv.z;
     s.w += bv.w;
+    return s;
+  };
+  // forward statistics about the block's first voxel (every thread of a
+  // channel group computes the same pivot; StatRow in common.h)
+  const bool fwdstat = a.stats && !a.bn_y;
+  const float4 piv = fwdstat ? vsum(v0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float cnt = 0.f;
+  for (int64_t v = v0 + tid / C4; v < v1; v += vstep) {
+    const size_t off = (size_t)v * a.OCs + c4 * 4;
+    float4 s = vsum(v);
     if (a.bn_y) {   // fused BatchNorm+ReLU backward: s = dA -> dz, stats (dz, dz*xhat)
       const int c = c4 * 4;
       const float4 yv = *reinterpret_cast<const float4 *>(a.bn_y + off);
@@ -566,27 +623,37 @@ __global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, in
       continue;
     }
     *reinterpret_cast<float4 *>(a.out + off) = s;
-    st1[0] += s.x; st1[1] += s.y; st1[2] += s.z; st1[3] += s.w;
-    st2[0] = fmaf(s.x, s.x, st2[0]);
-    st2[1] = fmaf(s.y, s.y, st2[1]);
-    st2[2] = fmaf(s.z, s.z, st2[2]);
-    st2[3] = fmaf(s.w, s.w, st2[3]);
+    const float d[4] = {s.x - piv.x, s.y - piv.y, s.z - piv.z, s.w - piv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      st1[j] += d[j];
+      st2[j] = fmaf(d[j], d[j], st2[j]);
+    }
+    cnt += 1.f;
   }
   if (!a.stats) return;
+  const float pk[4] = {piv.x, piv.y, piv.z, piv.w};
   for (int comp = 0; comp < 4; ++comp) {
     __syncthreads();
     red[tid][0] = st1[comp];
     red[tid][1] = st2[comp];
+    red[tid][2] = cnt;
     __syncthreads();
     if (tid < C4) {
-      float t1 = 0.f, t2 = 0.f;
+      float t1 = 0.f, t2 = 0.f, tn = 0.f;
       for (int k = tid; k < 256; k += C4) {
         t1 += red[k][0];
         t2 += red[k][1];
+        tn += red[k][2];
       }
       const int c = tid * 4 + comp;
-      a.stats[((size_t)blockIdx.x * a.CoutW + c) * 2 + 0] = t1;
-      a.stats[((size_t)blockIdx.x * a.CoutW + c) * 2 + 1] = t2;
+      if (fwdstat) {
+        *reinterpret_cast<float4 *>(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 4) =
+            make_float4(t1, t2, pk[comp], tn);
+      } else {
+        a.stats[((size_t)blockIdx.x * a.CoutW + c) * 2 + 0] = t1;
+        a.stats[((size_t)blockIdx.x * a.CoutW + c) * 2 + 1] = t2;
+      }
     }
   }
 }
@@ -619,8 +686,8 @@ static long conv2_lds(const GConvArgs &a, int CK, int NT) {
   const int T = a.KX * a.KY * a.KZ;
   const int TPS = 16 / CK;
   const int S = (T + TPS - 1) / TPS;
-  return std::max(conv2_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128,
-                  256L * 8) * 4;
+  return std::max(conv2_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128 + NT,
+                  256L * 12) * 4;
 }
 
 // Chooses CK / NSUB / MPW / tile / K split / prefetch depth / grid for
@@ -689,7 +756,7 @@ int plan_conv2(GConvArgs &a, int target_blocks) {
   a.nty = cdiv(a.OY, a.TY);
   a.ntz = ntz;
   if (!a.CK) return fail(4, "conv2: no tile fits in LDS");
-  if (a.lds_bytes < 4 * NT * 2 * 4) a.lds_bytes = 4 * NT * 2 * 4;
+  if (a.lds_bytes < 4 * NT * 3 * 4) a.lds_bytes = 4 * NT * 3 * 4;
   const long tiles = (long)a.ntx * a.nty * a.ntz * a.B;
   const int nchunks = a.ICs / a.CK;
   int ks = 1;

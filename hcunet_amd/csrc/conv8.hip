@@ -54,6 +54,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   int *toffs = reinterpret_cast<int *>(wlds + T * C4 * 32);      // [T] float offsets
   int *rowoff = toffs + T;                                       // [128*G] store offsets, -1 past MT
   int *rowpk = rowoff + 128 * G;                                  // [128*G] packed (lx,ly,lz)
+  float *pivl = reinterpret_cast<float *>(rowpk + 128 * G);       // [8] statistics pivot
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
 
@@ -97,7 +98,11 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   const float bnmu = (a.bn_y && cstat) ? a.bn_mean[col] : 0.f;
   const float bnis = (a.bn_y && cstat) ? a.bn_invstd[col] : 0.f;
   const float bias = (a.bias && cstat) ? a.bias[col] : 0.f;
-  float s1 = 0.f, s2 = 0.f;
+  // forward statistics about a block-wide pivot per channel (the value of the
+  // block's first output voxel; StatRow in common.h)
+  const bool fwdstat = a.stats && !a.bn_y;
+  float s1 = 0.f, s2 = 0.f, cnt = 0.f, piv = 0.f;
+  bool have_piv = false;
   const bool act = a.in_scale != nullptr;
   const int S = T * C4;
 
@@ -248,25 +253,34 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
           ro[g * 4 + rr] = in ? ro[g * 4 + rr] : -1;
         }
     }
+    if (fwdstat && !have_piv) {   // block-uniform: the first tile of this block
+      if (wave == 0 && ((lane >> 2) & 7) == 0) pivl[col] = acc[0][0] + bias;
+      __syncthreads();
+      piv = pivl[col];
+      have_piv = true;
+    }
 #pragma unroll
     for (int g = 0; g < ((a.dbg & 8) ? 0 : G); ++g) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int o = ro[g * 4 + rr];
         float v = acc[g][rr] + bias;
-        float w2 = v;
+        float w2 = v - piv, w1 = v - piv;
         if (a.bn_y) {   // fused BatchNorm+ReLU backward: v = dA -> dz, stats (dz, dz*xhat)
           const float yv = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(yrs, o >= 0 ? tbase + o * 4 : 0x7ffffff0, 0, 0));
           v = fmaf(yv, bnsc, bnsh) > 0.f ? v : 0.f;
+          w1 = v;
           w2 = (yv - bnmu) * bnis;
         }
         __builtin_amdgcn_raw_buffer_store_b32(
             __builtin_bit_cast(uint32_t, v), ors,
             (o >= 0 && cstore && !(a.dbg & 4)) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
-        const float w = (o >= 0 && cstat) ? v : 0.f;
+        const bool ok = o >= 0 && cstat;
+        const float w = ok ? w1 : 0.f;
         s1 += w;
         s2 = fmaf(w, w2, s2);
+        cnt += ok ? 1.f : 0.f;
       }
     }
   }
@@ -274,33 +288,43 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   // lanes sharing a channel differ in lane bits 2..4: fixed-order butterfly
   s1 += __shfl_xor(s1, 4);
   s2 += __shfl_xor(s2, 4);
+  cnt += __shfl_xor(cnt, 4);
   s1 += __shfl_xor(s1, 8);
   s2 += __shfl_xor(s2, 8);
+  cnt += __shfl_xor(cnt, 8);
   s1 += __shfl_xor(s1, 16);
   s2 += __shfl_xor(s2, 16);
+  cnt += __shfl_xor(cnt, 16);
   __syncthreads();
-  float *red = smem;  // [4 waves][8 channels][2]
+  float *red = smem;  // [4 waves][8 channels][3]
   if (((lane >> 2) & 7) == 0) {
-    red[(wave * 8 + col) * 2 + 0] = s1;
-    red[(wave * 8 + col) * 2 + 1] = s2;
+    red[(wave * 8 + col) * 3 + 0] = s1;
+    red[(wave * 8 + col) * 3 + 1] = s2;
+    red[(wave * 8 + col) * 3 + 2] = cnt;
   }
   __syncthreads();
   if (tid < 8) {
-    float t1 = 0.f, t2 = 0.f;
+    float t1 = 0.f, t2 = 0.f, tn = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      t1 += red[(w * 8 + tid) * 2 + 0];
-      t2 += red[(w * 8 + tid) * 2 + 1];
+      t1 += red[(w * 8 + tid) * 3 + 0];
+      t2 += red[(w * 8 + tid) * 3 + 1];
+      tn += red[(w * 8 + tid) * 3 + 2];
     }
-    a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 0] = t1;
-    a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 1] = t2;
+    if (fwdstat) {
+      *reinterpret_cast<float4 *>(a.stats + ((size_t)blockIdx.x * 8 + tid) * 4) =
+          make_float4(t1, t2, pivl[tid], tn);
+    } else {
+      a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 0] = t1;
+      a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 1] = t2;
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 static long conv8_lds(const GConvArgs &a, int C4, int HVP, int G) {
   const int T = a.KX * a.KY * a.KZ;
-  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G) * 4;
+  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G + 8) * 4;
 }
 
 // Chooses the tile, groups per wave and grid for conv8_kernel; non-zero when
@@ -348,7 +372,7 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
     a.HZr = HZr;
     a.HVP = HVP;
     a.NPF = HV * C4 <= 8 * 256 ? 8 : (HV * C4 <= 12 * 256 ? 12 : 16);
-    a.lds_bytes = (int)std::max(lds, 4L * 8 * 2 * 4);
+    a.lds_bytes = (int)std::max(lds, 4L * 8 * 3 * 4);
     found = true;
     if (tiles >= target_blocks / 2) break;
   }

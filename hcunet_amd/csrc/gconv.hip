@@ -140,15 +140,27 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
     }
   }
 
-  // ---- epilogue: bias, store, BatchNorm partial statistics
-  float s1[NSUB], s2[NSUB];
+  // ---- epilogue: bias, store, BatchNorm partial statistics (about a pivot per
+  // channel: the tile's first output voxel; StatRow in common.h)
+  float s1[NSUB], s2[NSUB], pv[NSUB], cnt = 0.f;
 #pragma unroll
-  for (int n = 0; n < NSUB; ++n) s1[n] = s2[n] = 0.f;
+  for (int n = 0; n < NSUB; ++n) s1[n] = s2[n] = pv[n] = 0.f;
   float bias_v[NSUB];
 #pragma unroll
   for (int n = 0; n < NSUB; ++n) {
     const int co = n0 + n * 16 + (lane & 15);
     bias_v[n] = (a.bias && co < a.Cout) ? a.bias[co] : 0.f;
+  }
+  float *pivl = smem + 4 * NT * 3;   // [NT], past the reduction area
+  if (a.stats) {
+    __syncthreads();   // every wave is done with the staged operands
+    if (wave == 0 && lane < 16) {
+#pragma unroll
+      for (int n = 0; n < NSUB; ++n) pivl[n * 16 + lane] = acc[0][n][0] + bias_v[n];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n) pv[n] = pivl[n * 16 + (lane & 15)];
   }
 #pragma unroll
   for (int j = 0; j < MPW; ++j) {
@@ -172,10 +184,12 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
               const float val = acc[j][n][r] + bias_v[n];
               if (co < a.OCs) a.out[ob + co] = val;
               if (co < a.Cout) {
-                s1[n] += val;
-                s2[n] = fmaf(val, val, s2[n]);
+                const float d = val - pv[n];
+                s1[n] += d;
+                s2[n] = fmaf(d, d, s2[n]);
               }
             }
+            cnt += 1.f;
           }
         }
       }
@@ -189,26 +203,30 @@ __global__ void __launch_bounds__(256) gconv_kernel(const GConvArgs a) {
       s2[n] += __shfl_xor(s2[n], 16);
       s2[n] += __shfl_xor(s2[n], 32);
     }
+    cnt += __shfl_xor(cnt, 16);
+    cnt += __shfl_xor(cnt, 32);
     __syncthreads();
-    float *red = smem;  // [4][NT][2]
+    float *red = smem;  // [4][NT][3]
     if (lane < 16) {
 #pragma unroll
       for (int n = 0; n < NSUB; ++n) {
-        red[(wave * NT + n * 16 + lane) * 2 + 0] = s1[n];
-        red[(wave * NT + n * 16 + lane) * 2 + 1] = s2[n];
+        red[(wave * NT + n * 16 + lane) * 3 + 0] = s1[n];
+        red[(wave * NT + n * 16 + lane) * 3 + 1] = s2[n];
+        red[(wave * NT + n * 16 + lane) * 3 + 2] = cnt;
       }
     }
     __syncthreads();
     if (tid < NT) {
-      float t1 = 0.f, t2 = 0.f;
+      float t1 = 0.f, t2 = 0.f, tn = 0.f;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
-        t1 += red[(w * NT + tid) * 2 + 0];
-        t2 += red[(w * NT + tid) * 2 + 1];
+        t1 += red[(w * NT + tid) * 3 + 0];
+        t2 += red[(w * NT + tid) * 3 + 1];
+        tn += red[(w * NT + tid) * 3 + 2];
       }
       const size_t row = (size_t)b * gridDim.x + blockIdx.x;
-      a.stats[(row * a.CoutW + n0 + tid) * 2 + 0] = t1;
-      a.stats[(row * a.CoutW + n0 + tid) * 2 + 1] = t2;
+      *reinterpret_cast<float4 *>(a.stats + (row * a.CoutW + n0 + tid) * 4) =
+          make_float4(t1, t2, pivl[tid], tn);
     }
   }
 }
@@ -278,7 +296,7 @@ int plan_gconv(GConvArgs &a, int target_blocks) {
   a.fHY = FastDiv(a.HY);
   a.fTZ = FastDiv(a.TZ);
   a.fTY = FastDiv(a.TY);
-  if (a.lds_bytes < 4 * NT * 2 * 4) a.lds_bytes = 4 * NT * 2 * 4;
+  if (a.lds_bytes < (4 * NT * 3 + NT) * 4) a.lds_bytes = (4 * NT * 3 + NT) * 4;
   return 0;
 }
 

@@ -29,29 +29,56 @@ __device__ __forceinline__ float comp(const float4 &v, int j) {
 
 // ---------------------------------------------------------------------------
 // BatchNorm forward finalisation: one workgroup per channel.
+//
+// Statistics rows (StatRow, common.h) hold sums taken about a per-row pivot K
+// (a value of the row's own data), so the fp32 partial sums never hold the
+// large (y - 0)^2 terms whose difference E[y^2] - E[y]^2 would cancel when
+// |mean| >> std (large conv biases, shifted inputs).  The rows are combined
+// here in fp64, in a fixed order, by the parallel-variance identity:
+//   mean = sum_r (S1_r + n_r K_r) / N
+//   M2   = sum_r (S2_r - S1_r^2 / n_r) + sum_r n_r (K_r + S1_r / n_r - mean)^2
+__device__ double block_sum_f64(double v, double *red) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  red[tid] = v;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  return red[0];
+}
+
 __global__ void __launch_bounds__(256)
 bn_fwd_finalize_kernel(const float *stats, int R, int W, int C, double count,
                        const float *gamma, const float *beta, float *rm, float *rv,
                        const int64_t *nbt, float eps, float momentum, int training,
                        BNCoef coef) {
-  __shared__ double r1[256], r2[256];
+  __shared__ double red[256];
   const int c = blockIdx.x, tid = threadIdx.x;
-  double s1 = 0.0, s2 = 0.0;
+  double m = 0.0, v = 0.0;
   if (training && c < C) {
+    double t = 0.0, nn = 0.0;
     for (int r = tid; r < R; r += 256) {
-      s1 += (double)stats[((size_t)r * W + c) * 2 + 0];
-      s2 += (double)stats[((size_t)r * W + c) * 2 + 1];
+      const float4 row = *reinterpret_cast<const float4 *>(stats + ((size_t)r * W + c) * 4);
+      if (row.w > 0.f) {
+        t += (double)row.x + (double)row.w * (double)row.z;
+        nn += (double)row.w;
+      }
     }
-  }
-  r1[tid] = s1;
-  r2[tid] = s2;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) {
-      r1[tid] += r1[tid + off];
-      r2[tid] += r2[tid + off];
+    const double tot = block_sum_f64(t, red);
+    const double ntot = block_sum_f64(nn, red);
+    m = tot / ntot;
+    double q = 0.0;
+    for (int r = tid; r < R; r += 256) {
+      const float4 row = *reinterpret_cast<const float4 *>(stats + ((size_t)r * W + c) * 4);
+      if (row.w > 0.f) {
+        const double n = row.w, s1 = row.x;
+        const double d = (double)row.z + s1 / n - m;
+        q += ((double)row.y - s1 * s1 / n) + n * d * d;
+      }
     }
-    __syncthreads();
+    v = block_sum_f64(q, red) / ntot;
   }
   if (tid != 0) return;
   if (c >= C) {
@@ -61,8 +88,6 @@ bn_fwd_finalize_kernel(const float *stats, int R, int W, int C, double count,
   }
   float mean, invstd;
   if (training) {
-    const double m = r1[0] / count;
-    double v = r2[0] / count - m * m;
     if (v < 0.0) v = 0.0;
     mean = (float)m;
     invstd = (float)(1.0 / sqrt(v + (double)eps));

@@ -370,7 +370,7 @@ size_t prep_floats_dgrad(const ConvLayer &L) { return wprep_floats(L.dgrad); }
 
 void track_conv(hcu_unet_plan &p, const ConvLayer &L) {
   p.max_act = std::max(p.max_act, std::max(L.in.floats(), L.out.floats()));
-  p.max_part = std::max(p.max_part, (size_t)gconv_rows(L.fwd) * L.fwd.CoutW * 2);
+  p.max_part = std::max(p.max_part, (size_t)gconv_rows(L.fwd) * L.fwd.CoutW * 4);  // StatRow
   p.max_part = std::max(p.max_part, wgrad_partial_floats(L.wg));
   p.max_part = std::max(p.max_part, (size_t)gconv_rows(L.dgrad) * L.dgrad.CoutW * 2);
   p.max_part = std::max(p.max_part, (size_t)bwd_rows(L.out.vox(), L.out.Cs) * L.out.Cs * 2);
@@ -800,6 +800,9 @@ int run_graphed(const hcu_unet_plan &p, std::vector<uintptr_t> key, hipStream_t 
   const hipError_t ce = hipStreamEndCapture(p.cap_stream, &graph);
   if (e || ce != hipSuccess) {
     if (graph) (void)hipGraphDestroy(graph);
+    // A failure after the backward forked its weight-gradient branch leaves
+    // the branch stream in an invalidated capture: recreate it on next use.
+    p.destroy_side();
     if (e) return e;
     return fail(HCU_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ce));
   }
@@ -862,6 +865,28 @@ int hcu_unet_plan_query(const hcu_unet_plan *p, int64_t *out_shape, int64_t *n_p
   if (saved_bytes) *saved_bytes = p->saved_bytes;
   if (scratch_bytes) *scratch_bytes = p->scratch_bytes;
   return HCU_OK;
+}
+
+int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int max) {
+  if (!p) return -fail(HCU_ERR_INVALID, "null plan");
+  std::vector<const ConvLayer *> ls(p->n_bn, nullptr);
+  for (const auto *v : {&p->dc1, &p->dc2, &p->uc1, &p->uc2})
+    for (const ConvLayer &L : *v) ls[L.bn.index] = &L;
+  for (int i = 0; i < p->n_bn && i < max && out; ++i) {
+    const ConvLayer &L = *ls[i];
+    hcu_bn_layer_info r{};
+    r.y_offset = (int64_t)L.y_off;
+    r.coef_offset = (int64_t)L.bn.coef_off;
+    r.B = L.out.B;
+    r.X = L.out.X;
+    r.Y = L.out.Y;
+    r.Z = L.out.Z;
+    r.C = L.out.C;
+    r.Cs = L.out.Cs;
+    r.elem_bytes = 4;
+    out[i] = r;
+  }
+  return p->n_bn;
 }
 
 static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,

@@ -72,6 +72,18 @@ class Adam(torch.optim.Optimizer):
                     s['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     s['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
 
+    # Any change of the optimizer's state or groups invalidates the cached flat
+    # layouts of _fast_step (a loaded state_dict replaces exp_avg/exp_avg_sq
+    # and 'step' with new tensors that the cached flat M/V would not update).
+    def load_state_dict(self, state_dict):
+        self._fast = {}
+        super().load_state_dict(state_dict)
+        self._fast = {}
+
+    def add_param_group(self, param_group):
+        self._fast = {}
+        super().add_param_group(param_group)
+
     def _fast_step(self, L, gi, group):
         """One launch for a group whose flat layout was verified on a previous
         step: re-checked with O(1) pointer tests instead of a pass over every
@@ -90,10 +102,24 @@ class Adam(torch.optim.Optimizer):
                 or pl.data_ptr() != pbase + 4 * (n - pl.numel())):
             fast.pop(gi, None)
             return False
-        # every parameter in between must also have a gradient (same flat buffer)
-        if any(p.grad is None for p in plist):
+        # every parameter in between must also have a gradient in the same flat
+        # buffer (a clone attached by a mixed-accumulation backward is not), and
+        # the optimizer state must still be the cached flat M/V and step tensor
+        s0, sl = self.state.get(p0), self.state.get(pl)
+        if (s0 is None or sl is None or s0.get('step') is not step_t
+                or sl.get('step') is not step_t
+                or s0['exp_avg'].data_ptr() != M.data_ptr()
+                or s0['exp_avg_sq'].data_ptr() != V.data_ptr()
+                or sl['exp_avg'].data_ptr() != M.data_ptr() + 4 * (n - pl.numel())):
             fast.pop(gi, None)
             return False
+        off = 0
+        for p in plist:
+            g = p.grad
+            if g is None or g.data_ptr() != gbase + 4 * off:
+                fast.pop(gi, None)
+                return False
+            off += p.numel()
         step = int(step_t.item()) + 1
         step_t.fill_(step)
         b1, b2 = group['betas']

@@ -345,6 +345,10 @@ class _Engine:
         self.plans = {}
         self.flat = None
         self.grad_flat = None
+        # grad_flat is the head of comm_flat; the tail is room for the BatchNorm
+        # running statistics, so a data-parallel step reduces both in ONE
+        # collective (hcunet_amd.dist.allreduce_gradients).
+        self.comm_flat = None
         self.params = None
         self._bn_arrays = None
 
@@ -369,8 +373,10 @@ class _Engine:
             self.plans[key] = p
         return p
 
-    def params_ready(self):
-        """Ensure every parameter is a view of one flat fp32 device buffer."""
+    def params_ready(self, require_gpu=True):
+        """Ensure every parameter is a view of one flat fp32 buffer (a device
+        buffer for the native path; require_gpu=False lays out host tensors the
+        same way, for the CPU tests of the data-parallel host logic)."""
         m = self.module_ref
         params = list(m.parameters())
         flat = self.flat
@@ -390,7 +396,8 @@ class _Engine:
                     raise RuntimeError('hcunet_amd: parameters must be float32')
                 if p.device != dev:
                     raise RuntimeError('hcunet_amd: parameters on several devices')
-            _lib.require_device(params[0], 'Unet_Constructor parameters')
+            if require_gpu:
+                _lib.require_device(params[0], 'Unet_Constructor parameters')
             n = sum(p.numel() for p in params)
             flat = torch.empty(n, dtype=torch.float32, device=dev)
             off = 0
@@ -403,6 +410,7 @@ class _Engine:
             self.flat = flat
             self.params = params
             self.grad_flat = None
+            self.comm_flat = None
             self._bn_arrays = None
         return self.params
 
@@ -446,7 +454,10 @@ class _Engine:
         params = self.params
         if self.grad_flat is None or self.grad_flat.numel() != self.flat.numel() \
                 or self.grad_flat.device != self.flat.device:
-            self.grad_flat = torch.zeros_like(self.flat)
+            n_stats = 2 * sum(bn.num_features for bn in bn_modules(self.module_ref))
+            self.comm_flat = torch.zeros(self.flat.numel() + n_stats, dtype=torch.float32,
+                                         device=self.flat.device)
+            self.grad_flat = self.comm_flat[:self.flat.numel()]
         G = self.grad_flat
         base = G.data_ptr()
         offs = []
@@ -494,8 +505,12 @@ class _UnetFunction(torch.autograd.Function):
             scratch.fill_(255)
         training = 1 if eng.module_ref.training else 0
         t = eng.tensors(x, out, saved, scratch)
-        _lib.check(_lib.lib().hcu_unet_forward(plan.handle, ctypes.byref(t), training,
-                                               _lib.stream_handle(dev)), 'Unet_Constructor.forward')
+        # The executor's graph-capture and side streams are created on the
+        # current device: make it the tensors' device.
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().hcu_unet_forward(plan.handle, ctypes.byref(t), training,
+                                                   _lib.stream_handle(dev)),
+                       'Unet_Constructor.forward')
         ctx.eng = eng
         ctx.plan = plan
         ctx.training = training
@@ -517,10 +532,11 @@ class _UnetFunction(torch.autograd.Function):
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         G, accumulate, finish = eng.grad_target()
         t = eng.tensors(x, None, saved, scratch, grads=G)
-        _lib.check(_lib.lib().hcu_unet_backward(plan.handle, ctypes.byref(t),
-                                                ctypes.c_void_p(dout.data_ptr()),
-                                                _lib.ptr(dx), ctx.training, accumulate,
-                                                _lib.stream_handle(dev)),
-                   'Unet_Constructor.backward')
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().hcu_unet_backward(plan.handle, ctypes.byref(t),
+                                                    ctypes.c_void_p(dout.data_ptr()),
+                                                    _lib.ptr(dx), ctx.training, accumulate,
+                                                    _lib.stream_handle(dev)),
+                       'Unet_Constructor.backward')
         finish()
         return (dx, None) + (None,) * len(eng.params)

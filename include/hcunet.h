@@ -12,11 +12,22 @@
  *
  * Conventions
  *   - Every pointer is a device (HBM) pointer owned by the caller.  No entry
- *     point allocates or frees memory; scratch/saved workspaces are sized by the
- *     *_bytes / *_query functions and passed in.
+ *     point allocates device memory for tensors; scratch/saved workspaces are
+ *     sized by the *_bytes / *_query functions and passed in.
  *   - Work is enqueued asynchronously on `stream` (a hipStream_t, 0 = null
- *     stream).  Launchers are re-entrant across streams: plans are read-only
- *     after creation.
+ *     stream).  The per-op launchers are stateless and re-entrant.
+ *   - A network plan (hcu_unet_plan) is NOT read-only after creation: on first
+ *     use it lazily creates, on the calling thread's current device, a private
+ *     capture stream and up to 8 instantiated hipGraphs per distinct set of
+ *     buffer pointers (guarded by a mutex), and for the backward a private
+ *     weight-gradient stream plus fork/join/slot events.  The backward enqueues
+ *     its weight-gradient branch on that private stream, ordered against the
+ *     caller's stream by events (fork after the caller's prior work, join before
+ *     the call returns its work to the caller's stream), so callers observe
+ *     ordinary stream order.  Concurrent backwards of one plan serialise on the
+ *     plan's mutex.  Call with the device of the tensors current (the Python
+ *     layer does).  A failed capture destroys the branch stream; it is
+ *     recreated on the next backward.
  *   - Return value: HCU_OK or an error code; no C++ exception crosses the ABI.
  *     hcu_last_error() returns a thread-local message for the last failure.
  *   - Activation tensors handled by the per-op entry points are channels-last
@@ -115,6 +126,21 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t,
 int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t,
                       const float *dout, float *dx, int training,
                       int accumulate, hcu_stream_t stream);
+
+/* Introspection of the saved workspace (tests, debugging): one record per
+ * BatchNorm3d in module order (down[i].batch1, batch2, ..., up[j].batch1,
+ * batch2).  y_offset: byte offset in `saved` of that layer's pre-BatchNorm conv
+ * output y, channels-last [B][X][Y][Z][Cs] of elem_bytes-sized elements;
+ * coef_offset: byte offset of 6 fp32 arrays of Cs (scale, shift, mean, invstd,
+ * c1, c0) with which the forward applied relu(y*scale + shift).  Returns the
+ * number of records (written up to max). */
+typedef struct hcu_bn_layer_info {
+  int64_t y_offset, coef_offset;
+  int B, X, Y, Z, C, Cs;
+  int elem_bytes;
+  int pad;
+} hcu_bn_layer_info;
+int hcu_unet_plan_bn_layers(const hcu_unet_plan *plan, hcu_bn_layer_info *out, int max);
 
 /* ------------------------------------------------------------------------ */
 /* Loss.  Replaces hcat.loss.cross_entropy(pred, mask, pwl, method='pixel')  */

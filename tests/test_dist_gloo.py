@@ -37,6 +37,7 @@ def _worker(rank, world, port, q):
     try:
         from hcat.unet import Unet_Constructor
         import hcunet_amd
+        from hcunet_amd.unet import bn_modules
         torch.manual_seed(rank)          # deliberately different init per rank
         m = Unet_Constructor(**KW)
         hcunet_amd.dist.broadcast_parameters(m)
@@ -51,15 +52,52 @@ def _worker(rank, world, port, q):
                              torch.from_numpy(inputs.make_pwl((4,) + ms[1:])[shard]))
         loss.backward()
         local = net.grads()
-        for n, p in m.named_parameters():   # hand the shard's grads to the module
-            p.grad = local[n].clone()
-        hcunet_amd.dist.allreduce_gradients(m)
+        # The production layout, exactly as a GPU backward leaves it: parameters
+        # are views of the engine's flat buffer and every .grad is a view of
+        # grad_flat, the head of the engine's communication buffer.
+        eng = m.engine()
+        eng.params_ready(require_gpu=False)
+        G, accumulate, finish = eng.grad_target()
+        assert accumulate == 0
+        off = 0
+        for n, p in m.named_parameters():
+            G[off:off + p.numel()].copy_(local[n].reshape(-1))
+            off += p.numel()
+        finish()
+        assert all(p.grad.data_ptr() == G.data_ptr() + 4 * o
+                   for p, o in zip(m.parameters(), _offsets(m)))
+        # per-shard running statistics after the train-mode forward (rank-local)
+        for bn, name in zip(bn_modules(m), uo.bn_names(spec)):
+            bn.running_mean.copy_(net.state[name + '.running_mean'])
+            bn.running_var.copy_(net.state[name + '.running_var'])
+        local_rs = {k: v.numpy().copy() for k, v in m.state_dict().items() if 'running' in k}
+        calls = []
+        real = dist.all_reduce
+
+        def counting_all_reduce(*a, **k):
+            calls.append(a[0].numel())
+            return real(*a, **k)
+        dist.all_reduce = counting_all_reduce
+        try:
+            hcunet_amd.dist.allreduce_gradients(m)
+        finally:
+            dist.all_reduce = real
         # numpy copies: tensors in a Queue would be shared with the exiting worker
         q.put((rank, {k: v.numpy().copy() for k, v in sd.items()},
                {n: p.grad.numpy().copy() for n, p in m.named_parameters()},
-               {n: g.numpy().copy() for n, g in local.items()}))
+               {n: g.numpy().copy() for n, g in local.items()},
+               {k: v.numpy().copy() for k, v in m.state_dict().items() if 'running' in k},
+               local_rs, calls, eng.comm_flat.data_ptr() == G.data_ptr()))
     finally:
         dist.destroy_process_group()
+
+
+def _offsets(m):
+    out, off = [], 0
+    for p in m.parameters():
+        out.append(off)
+        off += p.numel()
+    return out
 
 
 def test_dp_allreduce_matches_mean_of_shard_grads():
@@ -71,13 +109,19 @@ def test_dp_allreduce_matches_mean_of_shard_grads():
         p.start()
     res = {}
     for _ in range(2):
-        r, sd, red, local = q.get(timeout=300)
-        res[r] = tuple({k: torch.from_numpy(v) for k, v in d.items()} for d in (sd, red, local))
+        r, sd, red, local, rs, lrs, calls, headed = q.get(timeout=300)
+        res[r] = tuple({k: torch.from_numpy(v) for k, v in d.items()} for d in (sd, red, local, rs, lrs))
+        res[r] += (calls, headed)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    sd0, red0, loc0 = res[0]
-    sd1, red1, loc1 = res[1]
+    sd0, red0, loc0, rs0, lrs0, calls0, headed0 = res[0]
+    sd1, red1, loc1, rs1, lrs1, calls1, headed1 = res[1]
+    # ONE collective per step, over grads + running statistics, on the flat path
+    n_params = sum(v.numel() for v in loc0.values())
+    n_stats = sum(v.numel() for v in rs0.values())
+    assert calls0 == [n_params + n_stats] and calls1 == calls0
+    assert headed0 and headed1
     for k in sd0:   # broadcast made the replicas identical (rank 0's init)
         assert torch.equal(sd0[k], sd1[k]), k
     torch.manual_seed(0)
@@ -89,3 +133,8 @@ def test_dp_allreduce_matches_mean_of_shard_grads():
         mean = (loc0[n] + loc1[n]) / 2
         assert torch.allclose(red0[n], mean, rtol=1e-6, atol=1e-9), n
         assert torch.equal(red0[n], red1[n]), n
+    # running statistics: rank-symmetric after the step, = mean of the shards'
+    for k in rs0:
+        assert not torch.equal(lrs0[k], lrs1[k]) or 'var' in k, k   # shards differ
+        assert torch.equal(rs0[k], rs1[k]), k
+        assert torch.allclose(rs0[k], (lrs0[k] + lrs1[k]) / 2, rtol=1e-6, atol=1e-9), k

@@ -1,0 +1,63 @@
+"""The backward's launch modes give bitwise-identical results.
+
+HCU_SIDE (weight-gradient branch on its own stream) and HCU_GRAPHS (hipGraph
+capture/replay) are read once per process, so each mode runs in a child
+process started before any GPU call of its own: one with both off (serial,
+kernel-by-kernel on one stream), one with the defaults (graphs + split
+streams).  A missing event wait on the gradient-slot ring would make the
+split run read a slot the chain has already rewritten, which shows up as a
+bitwise difference in the gradients."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import sys, torch
+sys.path.insert(0, %(root)r)
+from hcat.unet import Unet_Constructor
+from hcat.loss import cross_entropy
+from oracle import inputs
+kw = dict(image_dimensions=3, in_channels=4, out_channels=1, feature_sizes=[8, 16, 32, 64, 128],
+          kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)}, upsample_kernel=(2, 2, 2),
+          max_pool_kernel=(2, 2, 1), upsample_stride=(2, 2, 1))
+torch.manual_seed(0)
+m = Unet_Constructor(**kw).cuda().train()
+x = torch.from_numpy(inputs.make_x((2, 4, 188, 188, 6))).cuda()
+res = []
+for it in range(3):          # 3 steps: the graphed mode replays its capture
+    for p in m.parameters():
+        p.grad = None
+    out = m(x)
+    ms = (2, 1) + tuple(out.shape[2:])
+    loss = cross_entropy(out, torch.from_numpy(inputs.make_mask(ms)).cuda(),
+                         torch.from_numpy(inputs.make_pwl(ms)).cuda(), method='pixel')
+    loss.backward()
+    res.append([out.detach().cpu()] + [p.grad.detach().cpu() for p in m.parameters()])
+torch.cuda.synchronize()
+torch.save(res, %(out)r)
+'''
+
+
+def _run(tmp_path, tag, env_extra):
+    out = str(tmp_path / ('%s.pt' % tag))
+    env = dict(os.environ)
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, '-c', CHILD % dict(root=ROOT, out=out)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return torch.load(out, weights_only=True)
+
+
+def test_split_graphed_equals_serial(tmp_path):
+    serial = _run(tmp_path, 'serial', {'HCU_SIDE': '0', 'HCU_GRAPHS': '0'})
+    split = _run(tmp_path, 'split', {'HCU_SIDE': '1', 'HCU_GRAPHS': '1'})
+    for it in range(3):
+        for a, b in zip(serial[it], split[it]):
+            assert torch.equal(a, b)
