@@ -1,0 +1,416 @@
+// bf16 weight gradient of Conv3d / ConvTranspose3d on v_mfma_f32_16x16x32_bf16.
+//
+//   Conv3d (taps on the rows):  dW[(t, ci)][co] = sum_p act(A[p + off(t)][ci]) * G[p][co]
+//                               (+ bias row: sum_p G[p][co])
+//   ConvTranspose3d (taps on the columns): dW[ci][(t, co)] = sum_p A[p][ci] * G[p*s + t][co]
+//
+// The reduction runs over voxels p, so both MFMA operands need 8 consecutive
+// VOXELS per lane, while activations live channels-last (8 consecutive
+// channels per 16 bytes).  Instead of transposing in a staging pass, the
+// channels-last tiles are staged as they come from HBM and every fragment is
+// read with ds_read_b64_tr_b16: a 16-lane group reads 4 voxel rows x 16
+// channel columns and each lane receives one channel of the 4 voxels.  Each
+// lane supplies its own row address, so the tap shift off(t) is just a per-lane
+// address offset into the A halo image (no per-tap image copies), and a row
+// subtile of 16 (tap, channel) pairs may straddle two taps when a tap has fewer
+// than 16 channels (first layer: 8 channel slots).
+//
+// Workgroup: 4 waves; the block owns a set of row subtiles (4*MSW, each wave
+// MSW of them) x NSB column subtiles of dW and a strided subset of the voxel
+// tiles (TX*TY*TZ voxels, TX*TY = 32 or 64 so every tile is a whole number of
+// 32-voxel K-steps; voxels outside the grid are staged as zero gradient).
+// Each wave keeps its own rows, so no cross-wave reduction is needed: every
+// block writes one fp32 partial slab and wgrad_finalize sums the slabs in fp64
+// in a fixed order (deterministic) and scatters them into the PyTorch layout.
+// Replaces the weight gradients of hcat/unet.py:246-257, 294-298 under
+// torch.autocast(dtype=torch.bfloat16).
+#include "common.h"
+#include "timing.h"
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace hcu {
+
+__device__ __forceinline__ shortx4 tr_read(const uint16_t *p) {
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s *)(
+          (__attribute__((address_space(3))) uint16_t *)(p)));
+}
+
+template <int MSW, int NS>
+__global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int T = a.KX * a.KY * a.KZ;
+  const int CKA = a.CKA, CKG = a.CKG, RSA = a.PA2, RSG = a.PG2;
+  int tapc, cic, coc;
+  if (a.taps_rows) {
+    tapc = blockIdx.y / a.nci;
+    cic = blockIdx.y % a.nci;
+    coc = blockIdx.z;
+  } else {
+    cic = blockIdx.y;
+    tapc = blockIdx.z / a.nco;
+    coc = blockIdx.z % a.nco;
+  }
+  const int ci0 = cic * CKA, co0 = coc * CKG;
+  const int t0 = tapc * (a.taps_rows ? a.TA : a.TG);
+  const bool bias_block = a.taps_rows && a.bias_row && tapc == 0 && cic == 0;
+  const int HAV = a.HAV, HGV = a.HGV, PT = a.PTV;
+  uint16_t *alds = reinterpret_cast<uint16_t *>(smem);          // [HAV][RSA]
+  uint16_t *glds = alds + (size_t)HAV * RSA;                    // [HGV][RSG]
+  int *hvA = reinterpret_cast<int *>(glds + (size_t)HGV * RSG);  // [PT] A row * RSA
+  int *hvG = hvA + PT;                                           // [PT] G row * RSG
+  const int HAZ = a.HAZ, HAYZ = a.HAY * a.HAZ, HGZ = a.HGZ, HGYZ = a.HGY * a.HGZ;
+
+  for (int p = tid; p < PT; p += 256) {
+    int q, lz, lx, ly;
+    a.fTZ.divmod(p, q, lz);
+    a.fTY.divmod(q, lx, ly);
+    hvA[p] = (lx * a.asx * HAYZ + ly * a.asy * HAZ + lz * a.asz) * RSA;
+    hvG[p] = (lx * a.gsx * HGYZ + ly * a.gsy * HGZ + lz * a.gsz) * RSG;
+  }
+  // per-lane column bases of this wave's row subtiles / the block's column
+  // subtiles (tap offset folded in); rows/cols past the block's extent read a
+  // valid address and are discarded at the write.
+  const int rows_blk = a.taps_rows ? a.TA * CKA : CKA;
+  const int cols_blk = a.taps_rows ? CKG : a.TG * CKG;
+  int colA[MSW], colG[NS];
+#pragma unroll
+  for (int m = 0; m < MSW; ++m) {
+    const int r = (wave + 4 * m) * 16 + 4 * p4;
+    int off = 0;
+    if (r < rows_blk) {
+      if (a.taps_rows) {
+        const int ta = t0 + r / CKA, c = r % CKA;
+        if (ta < T) {
+          const int kz = ta % a.KZ, qq = ta / a.KZ, ky = qq % a.KY, kx = qq / a.KY;
+          off = (kx * a.adx * HAYZ + ky * a.ady * HAZ + kz * a.adz) * RSA + c;
+        }
+      } else {
+        off = r;
+      }
+    }
+    colA[m] = off;
+  }
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+    const int c = n * 16 + 4 * p4;
+    int off = 0;
+    if (c < cols_blk) {
+      if (a.taps_rows) {
+        off = c;
+      } else {
+        const int tg = t0 + c / CKG, o = c % CKG;
+        if (tg < T) {
+          const int kz = tg % a.KZ, qq = tg / a.KZ, ky = qq % a.KY, kx = qq / a.KY;
+          off = (kx * a.gdx * HGYZ + ky * a.gdy * HGZ + kz * a.gdz) * RSG + o;
+        }
+      }
+    }
+    colG[n] = off;
+  }
+
+  floatx4 acc[MSW][NS], accb[NS];
+#pragma unroll
+  for (int m = 0; m < MSW; ++m)
+#pragma unroll
+    for (int n = 0; n < NS; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int n = 0; n < NS; ++n) accb[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = bias_block && wave == 0;
+  const shortx8 ones = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int CA8 = CKA / 8, CG8 = CKG / 8;
+  const bool act = a.a_scale != nullptr;
+  float sc[8], sh[8];
+  // activation of this thread's 8-channel A group (fixed: 256 % CA8 == 0)
+  {
+    const int c = ci0 + (tid % CA8) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sc[k] = act ? a.a_scale[c + k] : 1.f;
+      sh[k] = act ? a.a_shift[c + k] : 0.f;
+    }
+  }
+  const uint16_t *Ab = reinterpret_cast<const uint16_t *>(a.A);
+  const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
+
+  for (int tt = blockIdx.x; tt < total; tt += gridDim.x) {
+    const int b = tt / ntiles;
+    int tile = tt - b * ntiles;
+    const int tzi = tile % a.ntz;
+    tile /= a.ntz;
+    const int tyi = tile % a.nty, txi = tile / a.nty;
+    const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    __syncthreads();
+    {  // A halo (channels-last, activation applied, 0 outside the input)
+      const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
+      const size_t bbase = (size_t)b * a.AX * a.AY * a.AZ;
+      const int c8 = tid % CA8;
+      for (int v0 = tid / CA8; v0 < HAV; v0 += 4 * (256 / CA8)) {
+        uint4 val[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int v = v0 + u * (256 / CA8);
+          int q, hz, hx, hy;
+          a.fHAZ.divmod(v, q, hz);
+          a.fHAY.divmod(q, hx, hy);
+          const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+          ok[u] = v < HAV && (unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY &&
+                  (unsigned)gz < (unsigned)a.AZ;
+          val[u] = make_uint4(0u, 0u, 0u, 0u);
+          if (ok[u])
+            val[u] = *reinterpret_cast<const uint4 *>(
+                Ab + ((bbase + ((size_t)gx * a.AY + gy) * a.AZ + gz) * a.ACs + ci0 + c8 * 8));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int v = v0 + u * (256 / CA8);
+          if (v >= HAV) continue;
+          uint4 w = make_uint4(0u, 0u, 0u, 0u);
+          if (ok[u]) {
+            if (act) {
+              float f[8];
+              unpack8(val[u], f);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
+              w = pack8(f);
+            } else {
+              w = val[u];
+            }
+          }
+          *reinterpret_cast<uint4 *>(alds + (size_t)v * RSA + c8 * 8) = w;
+        }
+      }
+    }
+    {  // G image (channels-last, 0 outside the gradient's grid / the output grid)
+      const int gx0 = px0 * a.gsx - a.gpx, gy0 = py0 * a.gsy - a.gpy, gz0 = pz0 * a.gsz - a.gpz;
+      const size_t bbase = (size_t)b * a.GX * a.GY * a.GZ;
+      const int c8 = tid % CG8;
+      for (int v0 = tid / CG8; v0 < HGV; v0 += 4 * (256 / CG8)) {
+        uint4 val[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int v = v0 + u * (256 / CG8);
+          int q, hz, hx, hy;
+          a.fHGZ.divmod(v, q, hz);
+          a.fHGY.divmod(q, hx, hy);
+          const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+          // taps_rows: G is the output grid [PX][PY][PZ] (voxels past it are 0)
+          const bool ok = v < HGV && (unsigned)gx < (unsigned)a.GX && (unsigned)gy < (unsigned)a.GY &&
+                          (unsigned)gz < (unsigned)a.GZ &&
+                          (!a.taps_rows || (gx < a.PX && gy < a.PY && gz < a.PZ));
+          val[u] = make_uint4(0u, 0u, 0u, 0u);
+          if (ok)
+            val[u] = *reinterpret_cast<const uint4 *>(
+                Gb + ((bbase + ((size_t)gx * a.GY + gy) * a.GZ + gz) * a.GCs + co0 + c8 * 8));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int v = v0 + u * (256 / CG8);
+          if (v < HGV) *reinterpret_cast<uint4 *>(glds + (size_t)v * RSG + c8 * 8) = val[u];
+        }
+      }
+    }
+    // ConvTranspose3d: input voxels past the input grid must contribute 0; their
+    // A rows are 0 (staged as outside), so nothing else is needed.
+    __syncthreads();
+    for (int p0 = 0; p0 < PT; p0 += 32) {
+      const int pr = p0 + 8 * g + q4;
+      const int ra0 = hvA[pr], ra1 = hvA[pr + 4];
+      const int rg0 = hvG[pr], rg1 = hvG[pr + 4];
+      shortx8 bf[NS];
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        const shortx4 lo = tr_read(glds + rg0 + colG[n]);
+        const shortx4 hi = tr_read(glds + rg1 + colG[n]);
+        bf[n] = shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int m = 0; m < MSW; ++m) {
+        const shortx4 lo = tr_read(alds + ra0 + colA[m]);
+        const shortx4 hi = tr_read(alds + ra1 + colA[m]);
+        const shortx8 af = shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int n = 0; n < NS; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[n], acc[m][n], 0, 0, 0);
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int n = 0; n < NS; ++n)
+          accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bf[n], accb[n], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- one partial slab per block: each wave writes its own rows
+  const size_t slab = (size_t)blockIdx.x * a.Mtot;
+#pragma unroll
+  for (int m = 0; m < MSW; ++m) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = (wave + 4 * m) * 16 + g * 4 + r;
+      int grow = -1;
+      if (lr < rows_blk) {
+        if (a.taps_rows) {
+          const int ta = t0 + lr / CKA, ci = ci0 + lr % CKA;
+          if (ta < T && ci < a.ACs) grow = ta * a.ACs + ci;
+        } else if (ci0 + lr < a.ACs) {
+          grow = ci0 + lr;
+        }
+      }
+      if (grow < 0) continue;
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        const int lc = n * 16 + (lane & 15);
+        int gcol = -1;
+        if (lc < cols_blk) {
+          if (a.taps_rows) {
+            if (co0 + lc < a.GCs) gcol = co0 + lc;
+          } else {
+            const int tg = t0 + lc / CKG, o = co0 + lc % CKG;
+            if (tg < T && o < a.GCs) gcol = tg * a.GCs + o;
+          }
+        }
+        if (gcol >= 0) a.partial[(slab + grow) * a.Ntot + gcol] = acc[m][n][r];
+      }
+    }
+  }
+  if (do_bias && g == 0) {   // row 0 of the ones-subtile holds sum_p G[p][col]
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      const int lc = n * 16 + (lane & 15);
+      if (lc < CKG && co0 + lc < a.GCs)
+        a.partial[(slab + (size_t)T * a.ACs) * a.Ntot + co0 + lc] = accb[n][0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+int plan_bwgrad(WGradArgs &a, int target_blocks) {
+  a.use_bw = 0;
+  const int T = a.KX * a.KY * a.KZ;
+  if (a.ACs % 8 || a.GCs % 8) return fail(4, "bwgrad: channel strides must be multiples of 8");
+  if (a.PX <= 0 || a.PY <= 0 || a.PZ <= 0) return fail(2, "bwgrad: empty grid");
+  if (a.apx || a.apy || a.apz || a.gpx || a.gpy || a.gpz)
+    return fail(4, "bwgrad: padded operands are not supported");
+  // channel chunks: A side up to 32 channels, G side up to 64 (16-col subtiles)
+  a.CKA = std::min(a.ACs, 32);
+  if (a.ACs % a.CKA) a.CKA = 8;
+  a.CKG = std::min(a.GCs, 64);
+  if (a.GCs % a.CKG) a.CKG = (a.GCs % 32 == 0) ? 32 : (a.GCs % 16 == 0 ? 16 : 8);
+  const int ncol_tiles_full = a.taps_rows ? cdiv(a.CKG, 16) : 0;
+  // row / column subtiles per block
+  if (a.taps_rows) {
+    a.NSB = ncol_tiles_full;
+    const int rows_all = T * a.CKA;                    // all taps of one channel chunk
+    const int sub_all = cdiv(rows_all, 16);
+    int msw = cdiv(sub_all, 4);
+    if (msw > 9) msw = 5;                              // split the taps over blocks
+    a.MSW = msw <= 3 ? 3 : (msw <= 5 ? 5 : 9);
+    a.TA = std::min(T, (a.MSW * 4 * 16) / a.CKA);
+    if (a.TA < 1) return fail(4, "bwgrad: channel chunk too large");
+    a.TG = 1;
+    a.ntc = cdiv(T, a.TA);
+  } else {
+    // rows = input channels of one chunk (CKA / 16 subtiles), columns = (tap, co)
+    a.CKA = std::min(a.ACs, 64);
+    if (a.ACs % a.CKA) a.CKA = (a.ACs % 32 == 0) ? 32 : (a.ACs % 16 == 0 ? 16 : 8);
+    a.MSW = 1;
+    if (cdiv(a.CKA, 16) > 4 * a.MSW) return fail(4, "bwgrad: row chunk too large");
+    a.CKG = std::min(a.GCs, 32);
+    if (a.GCs % a.CKG) a.CKG = (a.GCs % 16 == 0) ? 16 : 8;
+    a.TG = std::max(1, std::min(T, 128 / a.CKG));      // up to 8 column subtiles
+    a.NSB = cdiv(a.TG * a.CKG, 16);
+    a.TA = 1;
+    a.ntc = cdiv(T, a.TG);
+  }
+  if (a.NSB > 8) return fail(4, "bwgrad: too many column subtiles");
+  a.nci = a.ACs / a.CKA;
+  a.nco = a.GCs / a.CKG;
+  a.mchunks = a.taps_rows ? a.ntc * a.nci : a.nci;
+  a.nchunks = a.taps_rows ? a.nco : a.ntc * a.nco;
+  a.Mtot = a.taps_rows ? T * a.ACs + (a.bias_row ? 1 : 0) : a.ACs;
+  a.Ntot = a.taps_rows ? a.GCs : T * a.GCs;
+  // voxel tile: TX*TY = 32 (or 64 when the halo fits), TZ = the whole Z (<= 16)
+  const int ntz = cdiv(a.PZ, 16);
+  a.TZ = cdiv(a.PZ, ntz);
+  a.PA2 = a.CKA + 8;
+  a.PG2 = a.CKG + 8;
+  const int txys[3][2] = {{8, 8}, {4, 8}, {4, 8}};
+  long lds = 0;
+  for (int i = 0; i < 3; ++i) {
+    a.TX = txys[i][0];
+    a.TY = txys[i][1];
+    a.HAX = (a.TX - 1) * a.asx + (a.taps_rows ? (a.KX - 1) * a.adx : 0) + 1;
+    a.HAY = (a.TY - 1) * a.asy + (a.taps_rows ? (a.KY - 1) * a.ady : 0) + 1;
+    a.HAZ = (a.TZ - 1) * a.asz + (a.taps_rows ? (a.KZ - 1) * a.adz : 0) + 1;
+    a.HGX = (a.TX - 1) * a.gsx + (a.taps_rows ? 0 : (a.KX - 1) * a.gdx) + 1;
+    a.HGY = (a.TY - 1) * a.gsy + (a.taps_rows ? 0 : (a.KY - 1) * a.gdy) + 1;
+    a.HGZ = (a.TZ - 1) * a.gsz + (a.taps_rows ? 0 : (a.KZ - 1) * a.gdz) + 1;
+    a.HAV = a.HAX * a.HAY * a.HAZ;
+    a.HGV = a.HGX * a.HGY * a.HGZ;
+    a.PTV = a.TX * a.TY * a.TZ;
+    lds = ((long)a.HAV * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
+    if (lds <= 80 * 1024) break;
+  }
+  if (lds > 160 * 1024) return fail(4, "bwgrad: tile does not fit LDS");
+  a.lds_bytes = (int)((lds + 15) & ~15L);
+  a.fHAZ = FastDiv(a.HAZ);
+  a.fHAY = FastDiv(a.HAY);
+  a.fHGZ = FastDiv(a.HGZ);
+  a.fHGY = FastDiv(a.HGY);
+  a.fTZ = FastDiv(a.TZ);
+  a.fTY = FastDiv(a.TY);
+  a.ntx = cdiv(a.PX, a.TX);
+  a.nty = cdiv(a.PY, a.TY);
+  a.ntz = ntz;
+  const long total = (long)a.B * a.ntx * a.nty * a.ntz;
+  const long per = (long)a.mchunks * a.nchunks;
+  a.occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
+  long kb = std::max(1L, (long)256 * a.occ / per);
+  kb = std::min(kb, total);
+  a.KB = (int)kb;
+  a.use_bw = 1;
+  a.v2 = 0;
+  if (getenv("HCU_CONV2_LOG"))
+    fprintf(stderr,
+            "bwgrad plan: rows%d A%dx%dx%d ACs%d G%dx%dx%d GCs%d P%dx%dx%d K%dx%dx%d | CKA%d CKG%d "
+            "TA%d TG%d MSW%d NSB%d T%dx%dx%d KB%d m%d n%d lds%d\n",
+            a.taps_rows, a.AX, a.AY, a.AZ, a.ACs, a.GX, a.GY, a.GZ, a.GCs, a.PX, a.PY, a.PZ, a.KX,
+            a.KY, a.KZ, a.CKA, a.CKG, a.TA, a.TG, a.MSW, a.NSB, a.TX, a.TY, a.TZ, a.KB, a.mchunks,
+            a.nchunks, a.lds_bytes);
+  (void)target_blocks;
+  return 0;
+}
+
+int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
+  const dim3 grid(a.KB, a.mchunks, a.nchunks);
+  const int T = a.KX * a.KY * a.KZ;
+  const double fl = a.flops > 0 ? a.flops
+                                : 2.0 * a.B * a.PX * a.PY * a.PZ * (double)T * a.ACs * a.GCs;
+  const double by = 2.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
+                           (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
+  bool ok = false;
+#define BW(MS_, NS_)                                                                        \
+  if (!ok && a.MSW == MS_ && a.NSB <= NS_) {                                                \
+    HCU_TIMED(s, "bwgrad_kernel<" #MS_ "," #NS_ ">", fl, by,                                  \
+              hipLaunchKernelGGL((bwgrad_kernel<MS_, NS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    ok = true;                                                                              \
+  }
+  BW(1, 1) BW(1, 2) BW(1, 4) BW(1, 8) BW(3, 1) BW(3, 2) BW(3, 4) BW(5, 1) BW(5, 2) BW(5, 4)
+  BW(9, 1) BW(9, 2) BW(9, 4)
+#undef BW
+  if (!ok) return fail(4, "bwgrad: unsupported variant");
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu

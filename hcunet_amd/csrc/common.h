@@ -7,8 +7,34 @@
 #include <string>
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));   // 8 bf16: one MFMA A/B fragment
+typedef short shortx4 __attribute__((ext_vector_type(4)));
 
 namespace hcu {
+
+// ---------------------------------------------------------------------------
+// bf16 storage helpers (the bf16 path keeps activations/gradients/weights in
+// bf16 and does all arithmetic in fp32; conversions round to nearest even via
+// v_cvt_pk_bf16_f32, which keeps NaNs NaN).
+__device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16 << 16); }
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a) |
+         ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+}
+__device__ __forceinline__ uint16_t f2bf(float a) {
+  return __builtin_bit_cast(unsigned short, (__bf16)a);
+}
+// 8 bf16 (one uint4) <-> 8 floats
+__device__ __forceinline__ void unpack8(const uint4 &v, float (&f)[8]) {
+  f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+  f[4] = bf_lo(v.z); f[5] = bf_hi(v.z); f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]),
+                    pack_bf2(f[6], f[7]));
+}
 
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
@@ -99,6 +125,9 @@ struct GConvArgs {
   // rows hold (sum dz, sum dz * (y-mean)*invstd) per channel.
   const float *bn_y, *bn_scale, *bn_shift, *bn_mean, *bn_invstd;
   double flops;                       // algorithmic FLOPs (0: derive)
+  // bconv (bconv.hip): the bf16 path.  in / out / bn_y / w point to bf16 data
+  // (channels-last activations, packed weights); partial stays fp32.
+  int use_bconv;
 };
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
 // (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n
@@ -134,18 +163,25 @@ inline int plan_conv_any(GConvArgs &a, int target_blocks) {
   a.use_conv8 = 0;
   return plan_gconv(a, target_blocks);
 }
+int plan_bconv(GConvArgs &a, int target_blocks);
+int launch_bconv(const GConvArgs &a, hipStream_t s);
+int bconv_stat_rows(const GConvArgs &a);
 inline int launch_conv_any(const GConvArgs &a, hipStream_t s) {
+  if (a.use_bconv) return launch_bconv(a, s);
   if (a.use_conv8) return launch_conv8(a, s);
   return a.use_conv2 ? launch_conv2(a, s) : launch_gconv(a, s);
 }
 inline int gconv_rows(const GConvArgs &a) {
+  if (a.use_bconv) return bconv_stat_rows(a);
   if (a.use_conv8) return a.gridx;
   return a.use_conv2 ? conv2_stat_rows(a) : a.B * a.ntx * a.nty * a.ntz;
 }
 // Whether the kernel planned in `a` supports the fused BatchNorm-backward epilogue.
-inline bool conv_bnbwd_fusable(const GConvArgs &a) { return a.use_conv8 || a.use_conv2; }
+inline bool conv_bnbwd_fusable(const GConvArgs &a) {
+  return a.use_conv8 || a.use_conv2 || a.use_bconv;
+}
 inline size_t conv_partial_floats(const GConvArgs &a) {
-  return (a.use_conv2 && !a.use_conv8) ? conv2_partial_floats(a) : 0;
+  return ((a.use_conv2 || a.use_bconv) && !a.use_conv8) ? conv2_partial_floats(a) : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -181,7 +217,13 @@ struct WGradArgs {
   // lane reads 4 consecutive voxels with one ds_read_b128; one A image per kz.
   int v2, TZP, HAZP, PA2, PG2, gridx, occ;
   double flops;                       // algorithmic FLOPs (0: derive)
+  // bwgrad (bwgrad.hip): the bf16 path (A, G bf16 channels-last); PA2 / PG2
+  // are the LDS row strides of the A halo / G images, MSW the row subtiles per
+  // wave, NSB the column subtiles of a block.
+  int use_bw, MSW, NSB, PTV, HAV, HGV;
 };
+int plan_bwgrad(WGradArgs &a, int target_blocks);
+int launch_bwgrad(const WGradArgs &a, hipStream_t s);
 int plan_wgrad(WGradArgs &a, int target_blocks);
 int launch_wgrad(const WGradArgs &a, hipStream_t s);
 inline size_t wgrad_partial_floats(const WGradArgs &a) {
@@ -224,47 +266,47 @@ int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, int W, doubl
 
 int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
                        float *p, int B, int X, int Y, int Z, int Cs,
-                       int kx, int ky, int kz, hipStream_t s);
+                       int kx, int ky, int kz, hipStream_t s, int bf = 0);
 
 // dz = dA * [relu'(z)] in place; partials [R][Cs][2] of (sum dz, sum dz*xhat).
 int bwd_rows(int64_t nvox, int Cs);
 int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef,
                                int64_t nvox, int Cs, float *part, int R,
-                               hipStream_t s);
+                               hipStream_t s, int bf = 0);
 // dz from a max-pool gradient dP (argmax recomputed from y); R = pool_bwd_rows(...).
 int pool_bwd_rows(int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz);
 int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef,
                               float *dz, int B, int X, int Y, int Z, int Cs,
                               int kx, int ky, int kz, float *part, int R,
-                              hipStream_t s);
+                              hipStream_t s, int bf = 0);
 // dy = dz*scale + c1*y + c0 in place.
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox,
-                        int Cs, hipStream_t s);
+                        int Cs, hipStream_t s, int bf = 0);
 
 // out_conv (1x1x1 Conv3d) forward: pred[b][o][v] (NCXYZ).
 int launch_outconv_fwd(const float *y, BNCoef coef, const float *w,
                        const float *bias, float *pred, int B, int64_t V, int C,
-                       int Cs, int Co, hipStream_t s);
+                       int Cs, int Co, hipStream_t s, int bf = 0);
 // out_conv backward fused with the last BatchNorm's backward reduction.
 int outconv_bwd_rows(int64_t nvox, int Cs);
 int launch_outconv_bwd(const float *dpred, const float *y, BNCoef coef,
                        const float *w, float *dz, int B, int64_t V, int C,
                        int Cs, int Co, float *part_bn, float *part_oc, int R,
-                       hipStream_t s);
+                       hipStream_t s, int bf = 0);
 
 // Channel sum of a channels-last tensor: partial [R][Cs].
 int chansum_rows(int64_t nvox, int Cs);
 int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R,
-                   hipStream_t s);
+                   hipStream_t s, int bf = 0);
 // out[j] (=|+=) sum_r part[r*W + j] for j < n, mapped: out index = j (dense).
 int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
                            int accumulate, hipStream_t s);
 
 // Layout: NCXYZ <-> channels-last (padded channels written as 0).
 int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V,
-                 hipStream_t s);
+                 hipStream_t s, int bf = 0, int x_dtype = 0);
 int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V,
-                   hipStream_t s);
+                   hipStream_t s, int bf = 0);
 
 // Weight preparation (PyTorch layout -> GEMM layouts).
 // Plain layout: wg[t][ci][co] (t < T, ci < ICs, co < CoutW).  Packed layout
@@ -278,6 +320,15 @@ struct WPack {
 };
 inline WPack wpack_of(const GConvArgs &a) {
   WPack p{};
+  if (a.use_bconv) {   // bf16 image wg[chunk][s][g][co][8] (bconv.hip), 32 K per step
+    const int T = a.KX * a.KY * a.KZ, TPS = 32 / a.CK;
+    p.on = 3;
+    p.CK = a.CK;
+    p.S = (T + TPS - 1) / TPS;
+    p.ICs = a.ICs;
+    p.CoutW = a.CoutW;
+    return p;
+  }
   if (a.use_conv8) {
     p.on = 2;
     p.CK = a.ICs / 4;
@@ -298,12 +349,14 @@ inline WPack wpack_of(const GConvArgs &a) {
 // Floats of the prepared weight buffer of a GEMM planned in `a`.
 // Elements of a prepared weight buffer (plain [T][ICs][CoutW] when !on).
 __host__ __device__ inline int64_t wpack_count(const WPack &p, int T, int ICs, int CoutW) {
+  if (p.on == 3) return (int64_t)p.ICs * p.S * (32 / p.CK) * p.CoutW;
   if (p.on == 2) return (int64_t)p.S * p.CK * 32;
   if (p.on) return (int64_t)p.ICs * p.S * (16 / p.CK) * p.CoutW;
   return (int64_t)T * ICs * CoutW;
 }
 inline size_t wprep_floats(const GConvArgs &a) {
   const int T = a.KX * a.KY * a.KZ;
+  if (a.use_bconv) return (size_t)(wpack_count(wpack_of(a), T, a.ICs, a.CoutW) + 1) / 2;
   if (a.use_conv8) return (size_t)T * a.ICs * 8;
   if (!a.use_conv2) return (size_t)T * a.ICs * a.CoutW;
   const WPack p = wpack_of(a);
@@ -312,6 +365,20 @@ inline size_t wprep_floats(const GConvArgs &a) {
 // Packed index -> (t, ci, co); false for a padded tap.
 __device__ __forceinline__ bool wpack_decode(const WPack &p, int64_t i, int T, int &t, int &ci,
                                              int &co) {
+  if (p.on == 3) {
+    const int j = (int)(i & 7);
+    int64_t q = i >> 3;
+    co = (int)(q % p.CoutW);
+    q /= p.CoutW;
+    const int g = (int)(q & 3);
+    q >>= 2;
+    const int s = (int)(q % p.S);
+    const int chunk = (int)(q / p.S);
+    const int C8 = p.CK / 8, TPS = 4 / C8;
+    t = s * TPS + g / C8;
+    ci = chunk * p.CK + (g % C8) * 8 + j;
+    return t < T;
+  }
   if (p.on == 2) {
     const int j = (int)(i & 3);
     co = (int)((i >> 2) & 7);
@@ -359,7 +426,7 @@ int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T,
 enum PrepKind { PREP_CONV_FWD = 0, PREP_CONV_DGRAD = 1, PREP_CONVT_FUSED = 2,
                 PREP_CONVT_PHASE = 3, PREP_CONVT_DGRAD = 4 };
 struct PrepJob {
-  int kind, pad;
+  int kind, bf16;   // bf16 != 0: the prepared image is written as bf16 (bconv)
   int64_t n;        // elements of the prepared buffer
   int64_t src;      // float offset of the PyTorch-layout weight in the parameter buffer
   int64_t dst;      // float offset of the prepared buffer in the destination workspace

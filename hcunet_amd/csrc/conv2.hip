@@ -492,22 +492,24 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     // fixed-order combine of the threads that share a channel group (they
     // share the pivot too, so their pivoted sums add)
     __syncthreads();
-    float *red = smem;  // [256][12]
-    red[tid * 12 + 0] = st1.x; red[tid * 12 + 1] = st1.y; red[tid * 12 + 2] = st1.z; red[tid * 12 + 3] = st1.w;
-    red[tid * 12 + 4] = st2.x; red[tid * 12 + 5] = st2.y; red[tid * 12 + 6] = st2.z; red[tid * 12 + 7] = st2.w;
-    red[tid * 12 + 8] = cnt;
+    float *red = smem;  // [256][16]: st1[4], st2[4], cnt, -, -, -, pivot[4]
+    red[tid * 16 + 0] = st1.x; red[tid * 16 + 1] = st1.y; red[tid * 16 + 2] = st1.z; red[tid * 16 + 3] = st1.w;
+    red[tid * 16 + 4] = st2.x; red[tid * 16 + 5] = st2.y; red[tid * 16 + 6] = st2.z; red[tid * 16 + 7] = st2.w;
+    red[tid * 16 + 8] = cnt;
+    red[tid * 16 + 12] = piv4.x; red[tid * 16 + 13] = piv4.y; red[tid * 16 + 14] = piv4.z; red[tid * 16 + 15] = piv4.w;
     __syncthreads();
     if (tid < nc4 * 4) {
       const int c4 = tid >> 2, comp = tid & 3;
       float t1 = 0.f, t2 = 0.f, tn = 0.f;
       for (int k = c4; k < 256; k += nc4) {
-        t1 += red[k * 12 + comp];
-        t2 += red[k * 12 + 4 + comp];
-        tn += red[k * 12 + 8];
+        t1 += red[k * 16 + comp];
+        t2 += red[k * 16 + 4 + comp];
+        tn += red[k * 16 + 8];
       }
       const size_t row = blockIdx.x;
       if (fwdstat) {
-        const float pk = comp == 0 ? piv4.x : (comp == 1 ? piv4.y : (comp == 2 ? piv4.z : piv4.w));
+        // thread c4 (< nc4) owns channel group c4: its pivot is this channel's
+        const float pk = red[c4 * 16 + 12 + comp];
         *reinterpret_cast<float4 *>(a.stats + (row * a.CoutW + n0 + tid) * 4) =
             make_float4(t1, t2, pk, tn);
       } else {
@@ -687,7 +689,7 @@ static long conv2_lds(const GConvArgs &a, int CK, int NT) {
   const int TPS = 16 / CK;
   const int S = (T + TPS - 1) / TPS;
   return std::max(conv2_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128 + NT,
-                  256L * 12) * 4;
+                  256L * 16) * 4;
 }
 
 // Chooses CK / NSUB / MPW / tile / K split / prefetch depth / grid for

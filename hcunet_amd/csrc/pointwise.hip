@@ -23,6 +23,33 @@ __device__ __forceinline__ float4 ld4(const float *p) {
 __device__ __forceinline__ void st4(float *p, float4 v) {
   *reinterpret_cast<float4 *>(p) = v;
 }
+// Activation storage types: the fp32 path stores float, the bf16 path bf16
+// (4 channels = 8 bytes); every kernel below computes in fp32 either way.
+struct bf16_t {
+  uint16_t v;
+};
+__device__ __forceinline__ float4 ld4(const bf16_t *p) {
+  const uint2 u = *reinterpret_cast<const uint2 *>(p);
+  return make_float4(bf_lo(u.x), bf_hi(u.x), bf_lo(u.y), bf_hi(u.y));
+}
+__device__ __forceinline__ void st4(bf16_t *p, float4 v) {
+  *reinterpret_cast<uint2 *>(p) = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
+}
+__device__ __forceinline__ float ld1(const float *p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t *p) { return bf2f(p->v); }
+__device__ __forceinline__ float ld1(const _Float16 *p) { return (float)*p; }
+__device__ __forceinline__ void st1(float *p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t *p, float v) { p->v = f2bf(v); }
+#define HCU_BF_DISPATCH(bf, KERNEL, ...)                     \
+  do {                                                       \
+    if (bf) {                                                \
+      using T = bf16_t;                                      \
+      hipLaunchKernelGGL(KERNEL<T>, __VA_ARGS__);            \
+    } else {                                                 \
+      using T = float;                                       \
+      hipLaunchKernelGGL(KERNEL<T>, __VA_ARGS__);            \
+    }                                                        \
+  } while (0)
 __device__ __forceinline__ float comp(const float4 &v, int j) {
   return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
@@ -177,8 +204,9 @@ int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, int W, doubl
 
 // ---------------------------------------------------------------------------
 // MaxPool3d forward on relu(bn(y)), kernel == stride, floor mode.
+template <typename T>
 __global__ void __launch_bounds__(256)
-maxpool_fwd_kernel(const float *y, const float *scale, const float *shift, float *p,
+maxpool_fwd_kernel(const T *y, const float *scale, const float *shift, T *p,
                    int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
                    int PX, int PY, int PZ) {
   const int C4 = Cs / 4;
@@ -229,11 +257,13 @@ static int grid_for(int64_t n) {
 
 int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
                        float *p, int B, int X, int Y, int Z, int Cs, int kx, int ky,
-                       int kz, hipStream_t s) {
+                       int kz, hipStream_t s, int bf) {
   const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
   const int64_t n = (int64_t)B * PX * PY * PZ * (Cs / 4);
-  HCU_TIMED(s, "maxpool_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, y, scale,
-                     shift, p, B, X, Y, Z, Cs, kx, ky, kz, PX, PY, PZ));
+  HCU_TIMED(s, "maxpool_fwd_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s,
+                            (const T *)y, scale, shift, (T *)p, B, X, Y, Z, Cs, kx, ky, kz, PX,
+                            PY, PZ));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -283,8 +313,9 @@ __device__ void block_reduce_c4(float (&v)[NV], float *lds, int tb, int C4,
 }
 
 // dz = dA * [z > 0] in place, partial (sum dz, sum dz*xhat) per channel.
+template <typename T>
 __global__ void __launch_bounds__(256)
-bn_bwd_reduce_dense_kernel(float *dA, const float *y, BNCoef coef, int64_t nvox,
+bn_bwd_reduce_dense_kernel(T *dA, const T *y, BNCoef coef, int64_t nvox,
                            int Cs, float *part, RedGeom g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int C4 = Cs / 4, tid = threadIdx.x;
@@ -319,10 +350,12 @@ bn_bwd_reduce_dense_kernel(float *dA, const float *y, BNCoef coef, int64_t nvox,
 }
 
 int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef, int64_t nvox,
-                               int Cs, float *part, int R, hipStream_t s) {
+                               int Cs, float *part, int R, hipStream_t s, int bf) {
   const RedGeom g = red_geom(nvox, Cs, R);
-  HCU_TIMED(s, "bn_bwd_reduce_dense_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_reduce_dense_kernel, dim3(R), dim3(256),
-                     (size_t)std::max(g.tb, 256) * 8 * 4, s, dA, y, coef, nvox, Cs, part, g));
+  HCU_TIMED(s, "bn_bwd_reduce_dense_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, bn_bwd_reduce_dense_kernel, dim3(R), dim3(256),
+                            (size_t)std::max(g.tb, 256) * 8 * 4, s, (T *)dA, (const T *)y, coef,
+                            nvox, Cs, part, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -333,8 +366,9 @@ int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef, int64_t n
 // once, and dz is written for the window's voxels plus, for windows on the
 // last row/column/plane, the floor-mode remainder (which gets 0), so every
 // voxel of y is written exactly once and y is read from HBM once.
+template <typename T>
 __global__ void __launch_bounds__(256)
-bn_bwd_reduce_pool_kernel(const float *dP, const float *y, BNCoef coef, float *dz,
+bn_bwd_reduce_pool_kernel(const T *dP, const T *y, BNCoef coef, T *dz,
                           int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
                           float *part, RedGeom g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -411,18 +445,20 @@ int pool_bwd_rows(int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz) {
 
 int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, float *dz,
                               int B, int X, int Y, int Z, int Cs, int kx, int ky,
-                              int kz, float *part, int R, hipStream_t s) {
+                              int kz, float *part, int R, hipStream_t s, int bf) {
   const RedGeom g = red_geom((int64_t)B * (X / kx) * (Y / ky) * (Z / kz), Cs, R);
-  HCU_TIMED(s, "bn_bwd_reduce_pool_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
-                     (size_t)std::max(g.tb, 256) * 8 * 4, s, dP, y, coef, dz, B, X, Y, Z,
-                     Cs, kx, ky, kz, part, g));
+  HCU_TIMED(s, "bn_bwd_reduce_pool_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
+                            (size_t)std::max(g.tb, 256) * 8 * 4, s, (const T *)dP, (const T *)y,
+                            coef, (T *)dz, B, X, Y, Z, Cs, kx, ky, kz, part, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
 
 // dy = dz*scale + c1*y + c0, in place.
+template <typename T>
 __global__ void __launch_bounds__(256)
-bn_bwd_apply_kernel(float *dz, const float *y, BNCoef coef, int64_t n4, int C4) {
+bn_bwd_apply_kernel(T *dz, const T *y, BNCoef coef, int64_t n4, int C4) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * 256) {
     const int c = (int)(i % C4) * 4;
@@ -438,10 +474,11 @@ bn_bwd_apply_kernel(float *dz, const float *y, BNCoef coef, int64_t n4, int C4) 
 }
 
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, int Cs,
-                        hipStream_t s) {
+                        hipStream_t s, int bf) {
   const int64_t n4 = nvox * (Cs / 4);
-  HCU_TIMED(s, "bn_bwd_apply_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, s, dz, y,
-                     coef, n4, Cs / 4));
+  HCU_TIMED(s, "bn_bwd_apply_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, bn_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, s,
+                            (T *)dz, (const T *)y, coef, n4, Cs / 4));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -449,8 +486,9 @@ int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, in
 // ---------------------------------------------------------------------------
 // out_conv forward: pred[b][o][v] = sum_c relu(bn(y))[v][c] * w[o][c] + bias[o]
 #define MAXCO 4
+template <typename T>
 __global__ void __launch_bounds__(256)
-outconv_fwd_kernel(const float *y, BNCoef coef, const float *w, const float *bias,
+outconv_fwd_kernel(const T *y, BNCoef coef, const float *w, const float *bias,
                    float *pred, int B, int64_t V, int C, int Cs, int Co) {
   const int64_t n = (int64_t)B * V;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
@@ -459,7 +497,7 @@ outconv_fwd_kernel(const float *y, BNCoef coef, const float *w, const float *bia
     const int64_t v = i % V;
     float acc[MAXCO];
     for (int o = 0; o < MAXCO; ++o) acc[o] = 0.f;
-    const float *yr = y + (size_t)i * Cs;
+    const T *yr = y + (size_t)i * Cs;
     for (int c0 = 0; c0 < Cs; c0 += 4) {
       const float4 yy = ld4(yr + c0);
       const float4 sc = ld4(coef.scale + c0), sh = ld4(coef.shift + c0);
@@ -478,10 +516,11 @@ outconv_fwd_kernel(const float *y, BNCoef coef, const float *w, const float *bia
 
 int launch_outconv_fwd(const float *y, BNCoef coef, const float *w, const float *bias,
                        float *pred, int B, int64_t V, int C, int Cs, int Co,
-                       hipStream_t s) {
+                       hipStream_t s, int bf) {
   if (Co > MAXCO) return fail(4, "out_conv: out_channels > 4 not supported");
-  HCU_TIMED(s, "outconv_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_fwd_kernel, dim3(grid_for((int64_t)B * V)), dim3(256), 0, s,
-                     y, coef, w, bias, pred, B, V, C, Cs, Co));
+  HCU_TIMED(s, "outconv_fwd_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, outconv_fwd_kernel, dim3(grid_for((int64_t)B * V)), dim3(256), 0,
+                            s, (const T *)y, coef, w, bias, pred, B, V, C, Cs, Co));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -490,9 +529,10 @@ int launch_outconv_fwd(const float *y, BNCoef coef, const float *w, const float 
 //   dA[v][c] = sum_o dpred[o][v] w[o][c];  dz = dA [z>0];
 //   part_bn[r][c][2] = (sum dz, sum dz*xhat);
 //   part_oc[r][o*Cs + c] = sum dpred[o] a[c];  part_oc[r][Co*Cs + o] = sum dpred[o]
+template <typename T>
 __global__ void __launch_bounds__(256)
-outconv_bwd_kernel(const float *dpred, const float *y, BNCoef coef, const float *w,
-                   float *dz, int B, int64_t V, int C, int Cs, int Co, float *part_bn,
+outconv_bwd_kernel(const float *dpred, const T *y, BNCoef coef, const float *w,
+                   T *dz, int B, int64_t V, int C, int Cs, int Co, float *part_bn,
                    float *part_oc, RedGeom g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int NV = 8 + 5 * MAXCO;
@@ -559,19 +599,22 @@ outconv_bwd_kernel(const float *dpred, const float *y, BNCoef coef, const float 
 
 int launch_outconv_bwd(const float *dpred, const float *y, BNCoef coef, const float *w,
                        float *dz, int B, int64_t V, int C, int Cs, int Co, float *part_bn,
-                       float *part_oc, int R, hipStream_t s) {
+                       float *part_oc, int R, hipStream_t s, int bf) {
   if (Co > MAXCO) return fail(4, "out_conv: out_channels > 4 not supported");
   const RedGeom g = red_geom((int64_t)B * V, Cs, R);
   const size_t lds = (size_t)std::max(g.tb, 256) * (8 + 5 * MAXCO) * 4;
-  HCU_TIMED(s, "outconv_bwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_bwd_kernel, dim3(R), dim3(256), lds, s, dpred, y, coef, w,
-                     dz, B, V, C, Cs, Co, part_bn, part_oc, g));
+  HCU_TIMED(s, "outconv_bwd_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, outconv_bwd_kernel, dim3(R), dim3(256), lds, s, dpred,
+                            (const T *)y, coef, w, (T *)dz, B, V, C, Cs, Co, part_bn, part_oc,
+                            g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
 
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void __launch_bounds__(256)
-chansum_kernel(const float *x, int Cs, float *part, RedGeom g) {
+chansum_kernel(const T *x, int Cs, float *part, RedGeom g) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int C4 = Cs / 4, tid = threadIdx.x;
   float v[4] = {0, 0, 0, 0};
@@ -589,10 +632,12 @@ chansum_kernel(const float *x, int Cs, float *part, RedGeom g) {
   block_reduce_c4<4>(v, lds, g.tb, C4, part + (size_t)blockIdx.x * Cs);
 }
 
-int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R, hipStream_t s) {
+int launch_chansum(const float *x, int64_t nvox, int Cs, float *part, int R, hipStream_t s,
+                   int bf) {
   const RedGeom g = red_geom(nvox, Cs, R);
-  HCU_TIMED(s, "chansum_kernel", 0.0, 0.0, hipLaunchKernelGGL(chansum_kernel, dim3(R), dim3(256), (size_t)std::max(g.tb, 256) * 4 * 4,
-                     s, x, Cs, part, g));
+  HCU_TIMED(s, "chansum_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, chansum_kernel, dim3(R), dim3(256),
+                            (size_t)std::max(g.tb, 256) * 4 * 4, s, (const T *)x, Cs, part, g));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -629,8 +674,9 @@ int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
 }
 
 // ---------------------------------------------------------------------------
+template <typename TI, typename T>
 __global__ void __launch_bounds__(256)
-to_cl_kernel(const float *x, float *xcl, int B, int C, int Cs, int64_t V) {
+to_cl_kernel(const TI *x, T *xcl, int B, int C, int Cs, int64_t V) {
   const int C4 = Cs / 4;
   const int64_t n = (int64_t)B * C4 * V;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
@@ -642,21 +688,46 @@ to_cl_kernel(const float *x, float *xcl, int B, int C, int Cs, int64_t V) {
     float r[4];
     for (int j = 0; j < 4; ++j) {
       const int c = c4 * 4 + j;
-      r[j] = c < C ? x[((size_t)b * C + c) * V + v] : 0.f;
+      r[j] = c < C ? ld1(x + ((size_t)b * C + c) * V + v) : 0.f;
     }
     st4(xcl + ((size_t)b * V + v) * Cs + c4 * 4, make_float4(r[0], r[1], r[2], r[3]));
   }
 }
 
-int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s) {
+// x_dtype: HCU_F32 / HCU_F16 / 3 = bf16 input volume; bf: bf16 channels-last output.
+int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s,
+                 int bf, int x_dtype) {
   const int64_t n = (int64_t)B * (Cs / 4) * V;
-  HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0, hipLaunchKernelGGL(to_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, xcl, B, C, Cs, V));
+  const dim3 gr(grid_for(n));
+  if (x_dtype == 1 && bf)
+    HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
+              hipLaunchKernelGGL((to_cl_kernel<_Float16, bf16_t>), gr, dim3(256), 0, s,
+                                 (const _Float16 *)x, (bf16_t *)xcl, B, C, Cs, V));
+  else if (x_dtype == 3 && bf)
+    HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
+              hipLaunchKernelGGL((to_cl_kernel<bf16_t, bf16_t>), gr, dim3(256), 0, s,
+                                 (const bf16_t *)x, (bf16_t *)xcl, B, C, Cs, V));
+  else if (x_dtype == 0 && bf)
+    HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
+              hipLaunchKernelGGL((to_cl_kernel<float, bf16_t>), gr, dim3(256), 0, s, x,
+                                 (bf16_t *)xcl, B, C, Cs, V));
+  else if (x_dtype == 1)
+    HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
+              hipLaunchKernelGGL((to_cl_kernel<_Float16, float>), gr, dim3(256), 0, s,
+                                 (const _Float16 *)x, xcl, B, C, Cs, V));
+  else if (x_dtype == 0)
+    HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
+              hipLaunchKernelGGL((to_cl_kernel<float, float>), gr, dim3(256), 0, s, x, xcl, B, C,
+                                 Cs, V));
+  else
+    return fail(4, "to_cl: unsupported input dtype");
   HCU_CHECK_LAUNCH();
   return 0;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-from_cl_kernel(const float *xcl, float *x, int B, int C, int Cs, int64_t V) {
+from_cl_kernel(const T *xcl, float *x, int B, int C, int Cs, int64_t V) {
   const int64_t n = (int64_t)B * C * V;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
@@ -664,13 +735,16 @@ from_cl_kernel(const float *xcl, float *x, int B, int C, int Cs, int64_t V) {
     const int64_t q = i / V;
     const int c = (int)(q % C);
     const int b = (int)(q / C);
-    x[i] = xcl[((size_t)b * V + v) * Cs + c];
+    x[i] = ld1(xcl + ((size_t)b * V + v) * Cs + c);
   }
 }
 
-int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V, hipStream_t s) {
+int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V, hipStream_t s,
+                   int bf) {
   const int64_t n = (int64_t)B * C * V;
-  HCU_TIMED(s, "from_cl_kernel", 0.0, 0.0, hipLaunchKernelGGL(from_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s, xcl, x, B, C, Cs, V));
+  HCU_TIMED(s, "from_cl_kernel", 0.0, 0.0,
+            HCU_BF_DISPATCH(bf, from_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s,
+                            (const T *)xcl, x, B, C, Cs, V));
   HCU_CHECK_LAUNCH();
   return 0;
 }

@@ -97,6 +97,13 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
   const PrepJob &jb = b.j[blockIdx.y];
   const float *w = params + jb.src;
   float *dst = dst_base + jb.dst;
+  if (jb.bf16) {
+    uint16_t *d16 = reinterpret_cast<uint16_t *>(dst);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < jb.n;
+         i += (int64_t)gridDim.x * 256)
+      d16[i] = f2bf(prep_value(jb, w, i));
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < jb.n;
        i += (int64_t)gridDim.x * 256)
     dst[i] = prep_value(jb, w, i);
