@@ -36,6 +36,7 @@ from hcunet_amd import _lib  # noqa: E402
 
 METRIC = "training voxels/sec (fwd+bwd+step), 5-level 3D U-Net, 256×256×16×4 tiles"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, dense
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA, dense (no sparsity)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E spec
 TILE = (256, 256, 16)
 
@@ -45,8 +46,18 @@ CONFIGS = {
                       kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)},
                       upsample_kernel=(2, 2, 2), max_pool_kernel=(2, 2, 1),
                       upsample_stride=(2, 2, 1)),
-              batch=2, dtype='fp32',
-              desc='3D U-Net feature_sizes=[8,16,32,64,128] fp32'),
+              batch=2, dtype='fp32', roof_ms=0.351,
+              desc='config 2: 3D U-Net feature_sizes=[8,16,32,64,128] fp32'),
+    # BASELINE config 3: [32..512], B=4, bf16 (torch.autocast bf16 -> the bf16
+    # MFMA path: bf16 activations/gradients/operands, fp32 accumulation, BN
+    # statistics, master weights and Adam state).
+    '3': dict(kw=dict(image_dimensions=3, in_channels=4, out_channels=1,
+                      feature_sizes=[32, 64, 128, 256, 512],
+                      kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)},
+                      upsample_kernel=(2, 2, 2), max_pool_kernel=(2, 2, 1),
+                      upsample_stride=(2, 2, 1)),
+              batch=4, dtype='bf16', roof_ms=0.891,
+              desc='config 3: 3D U-Net feature_sizes=[32,64,128,256,512] bf16 (autocast)'),
     # BASELINE config 3's shapes ([32..512], B=4) computed in fp32: the bf16
     # path is not built, so this is a capacity/shape check, not config 3 itself.
     '3f32': dict(kw=dict(image_dimensions=3, in_channels=4, out_channels=1,
@@ -54,7 +65,7 @@ CONFIGS = {
                          kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)},
                          upsample_kernel=(2, 2, 2), max_pool_kernel=(2, 2, 1),
                          upsample_stride=(2, 2, 1)),
-                 batch=4, dtype='fp32',
+                 batch=4, dtype='fp32', roof_ms=None,
                  desc='3D U-Net feature_sizes=[32,64,128,256,512] fp32 (config-3 shapes)'),
 }
 
@@ -90,7 +101,8 @@ def cpu_baseline(cfg, x, mask, pwl, budget_s=15.0):
     vox = x.shape[0] * TILE[0] * TILE[1] * TILE[2]
     return {"value": vox / med, "unit": "voxels/s", "cores": threads, "kind": "port",
             "sample": "%d full train steps (B=%d, fwd+loss+bwd+Adam) of the oracle "
-                      "restatement (torch CPU, %d threads), median %.3f s/step"
+                      "restatement of the reference (torch CPU fp32 -- the reference's own "
+                      "arithmetic; it has no bf16 path -- %d threads), median %.3f s/step"
                       % (len(times), x.shape[0], threads, med)}
 
 
@@ -132,10 +144,13 @@ def main():
     opt = hcunet_amd.optim.Adam(model.parameters(), lr=1e-3)
     x, mask, pwl = synth_inputs(B, 1000 + rank, device)
 
+    bf16 = cfg['dtype'] == 'bf16'
+
     def step():
         opt.zero_grad()
-        out = model(x)
-        loss = cross_entropy(out, mask, pwl, method='pixel')
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=bf16):
+            out = model(x)
+            loss = cross_entropy(out, mask, pwl, method='pixel')
         loss.backward()
         hcunet_amd.dist.allreduce_gradients(model)
         opt.step()
@@ -177,7 +192,9 @@ def main():
         avg_s = d['ms'] / d['count'] / 1e3
         if d['flops'] > 0:
             ach = d['flops'] / d['count'] / avg_s / 1e12
-            bound, peak, unit = 'mfma', PEAK_FP32_MFMA_TFLOPS, 'TFLOP/s'
+            bf_kernel = name.startswith(('bconv', 'bwgrad'))
+            bound, unit = 'mfma', 'TFLOP/s'
+            peak = PEAK_BF16_MFMA_TFLOPS if bf_kernel else PEAK_FP32_MFMA_TFLOPS
         else:
             ach = d['bytes'] / d['count'] / avg_s / 1e9
             bound, peak, unit = 'hbm', PEAK_HBM_GBS, 'GB/s'
@@ -210,6 +227,12 @@ def main():
                            "global_batch": B * world, "per_gpu_batch": B,
                            "parallelism": "dp%d" % world, "final_loss": final_loss},
                 "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
+        if cfg.get('roof_ms'):
+            # SURVEY §8d per-layer roofline of the whole step (sum over layers of
+            # max(bytes / 8 TB/s, flops / dense MFMA peak)) vs the measured step
+            line["step_roofline"] = {"per_layer_roofline_ms": cfg['roof_ms'],
+                                     "measured_ms": ms_per_step,
+                                     "frac": cfg['roof_ms'] / ms_per_step}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -18,7 +18,7 @@ HCU_ERR_HIP = 3
 HCU_ERR_UNSUPPORTED = 4
 HCU_ERR_WORKSPACE = 5
 
-HCU_F32, HCU_F16, HCU_U8 = 0, 1, 2
+HCU_F32, HCU_F16, HCU_U8, HCU_BF16 = 0, 1, 2, 3
 MAX_LEVELS = 12
 
 c_int3 = ctypes.c_int * 3
@@ -37,6 +37,7 @@ class UnetSpec(ctypes.Structure):
         ("pool_k", c_int3),
         ("bn_eps", ctypes.c_float),
         ("bn_momentum", ctypes.c_float),
+        ("compute_dtype", ctypes.c_int),
     ]
 
 
@@ -51,6 +52,7 @@ class UnetTensors(ctypes.Structure):
         ("bn_num_batches_tracked", ctypes.POINTER(ctypes.c_void_p)),
         ("saved", ctypes.c_void_p),
         ("scratch", ctypes.c_void_p),
+        ("x_dtype", ctypes.c_int),
     ]
 
 
@@ -61,6 +63,7 @@ class ConvDesc(ctypes.Structure):
         ("k", c_int3), ("stride", c_int3), ("dil", c_int3),
         ("groups", ctypes.c_int),
         ("transposed", ctypes.c_int),
+        ("dtype", ctypes.c_int),
     ]
 
 

@@ -325,7 +325,9 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
     if (a.ACs % a.CKA) a.CKA = (a.ACs % 32 == 0) ? 32 : (a.ACs % 16 == 0 ? 16 : 8);
     a.MSW = 1;
     if (cdiv(a.CKA, 16) > 4 * a.MSW) return fail(4, "bwgrad: row chunk too large");
-    a.CKG = std::min(a.GCs, 32);
+    // the G operand is a strided halo (~S^2 (TZ+1)/TZ rows per voxel): keep
+    // its channel chunk small so the image fits LDS
+    a.CKG = std::min(a.GCs, (a.gsx * a.gsy * a.gsz > 1) ? 16 : 32);
     if (a.GCs % a.CKG) a.CKG = (a.GCs % 16 == 0) ? 16 : 8;
     a.TG = std::max(1, std::min(T, 128 / a.CKG));      // up to 8 column subtiles
     a.NSB = cdiv(a.TG * a.CKG, 16);

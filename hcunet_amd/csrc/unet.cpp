@@ -45,20 +45,24 @@ namespace {
 
 constexpr int kTargetBlocks = 1024;
 
+// Activation tensor dims.  es = element bytes: 4 (fp32 path, channel stride a
+// multiple of 4 = 16 bytes) or 2 (bf16 path, channel stride a multiple of 8).
 struct Dims {
-  int B = 0, X = 0, Y = 0, Z = 0, C = 0, Cs = 0;
+  int B = 0, X = 0, Y = 0, Z = 0, C = 0, Cs = 0, es = 4;
   int64_t vox() const { return (int64_t)B * X * Y * Z; }
-  size_t floats() const { return (size_t)vox() * Cs; }
+  // 4-byte slots the tensor occupies (buffers are carved in float units)
+  size_t floats() const { return ((size_t)vox() * Cs * es + 3) / 4; }
 };
 
-Dims mkdims(int B, int X, int Y, int Z, int C) {
+Dims mkdims(int B, int X, int Y, int Z, int C, int es) {
   Dims d;
   d.B = B;
   d.X = X;
   d.Y = Y;
   d.Z = Z;
   d.C = C;
-  d.Cs = round_up(C, 4);
+  d.es = es;
+  d.Cs = round_up(C, es == 2 ? 8 : 4);
   return d;
 }
 
@@ -185,13 +189,15 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
                                    std::to_string(in.X) + " x " + std::to_string(in.Y) + " x " +
                                    std::to_string(in.Z) +
                                    "). Kernel size can't be greater than actual input size");
-  L.out = mkdims(in.B, ox, oy, oz, Cout);
+  L.out = mkdims(in.B, ox, oy, oz, Cout, in.es);
+  const bool bf = in.es == 2;
   L.fwd = gconv_conv_fwd(in, L.out, K, D, Cout);
-  if (int e = plan_conv_any(L.fwd, kTargetBlocks)) return e;
+  if (int e = bf ? plan_bconv(L.fwd, kTargetBlocks) : plan_conv_any(L.fwd, kTargetBlocks)) return e;
   L.dgrad = gconv_conv_dgrad(in, L.out, K, D, L.E);
-  if (int e = plan_conv_any(L.dgrad, kTargetBlocks)) return e;
+  if (int e = bf ? plan_bconv(L.dgrad, kTargetBlocks) : plan_conv_any(L.dgrad, kTargetBlocks))
+    return e;
   L.wg = wgrad_conv(in, L.out, K, D);
-  if (int e = plan_wgrad(L.wg, kTargetBlocks)) return e;
+  if (int e = bf ? plan_bwgrad(L.wg, kTargetBlocks) : plan_wgrad(L.wg, kTargetBlocks)) return e;
   L.bn.C = Cout;
   L.bn.Cs = L.out.Cs;
   L.bn.count = (double)L.out.vox();
@@ -213,11 +219,15 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
   u.in = cur;
   const int ux = (cur.X - 1) * u.S[0] + u.K[0], uy = (cur.Y - 1) * u.S[1] + u.K[1],
             uz = (cur.Z - 1) * u.S[2] + u.K[2];
-  u.out = mkdims(cur.B, ux, uy, uz, o);
+  u.out = mkdims(cur.B, ux, uy, uz, o, cur.es);
+  const bool bf = cur.es == 2;
   u.phases.clear();
   u.pJ.clear();
   const int nph = u.S[0] * u.S[1] * u.S[2];
   u.fused = u.K[0] % u.S[0] == 0 && u.K[1] % u.S[1] == 0 && u.K[2] % u.S[2] == 0;
+  if (bf && !u.fused)
+    return fail(HCU_ERR_UNSUPPORTED,
+                "ConvTranspose3d with kernel % stride != 0 is not supported on the bf16 path");
   if (u.fused) {
     const int Jx = u.K[0] / u.S[0], Jy = u.K[1] / u.S[1], Jz = u.K[2] / u.S[2];
     GConvArgs a{};
@@ -231,7 +241,12 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     a.dx = a.dy = a.dz = 1;
     a.px = Jx - 1; a.py = Jy - 1; a.pz = Jz - 1;
     a.nph = nph; a.phx = u.S[0]; a.phy = u.S[1]; a.phz = u.S[2];
-    if (plan_conv2(a, kTargetBlocks) == 0) {
+    if (bf) {
+      if (int e = plan_bconv(a, kTargetBlocks)) return e;
+      u.fwdf = a;
+      max_wprep = std::max(max_wprep, wprep_floats(a));
+      max_kpart = std::max(max_kpart, conv_partial_floats(a));
+    } else if (plan_conv2(a, kTargetBlocks) == 0) {
       u.fwdf = a;
       max_wprep = std::max(max_wprep, wprep_floats(a));
       max_kpart = std::max(max_kpart, conv_partial_floats(a));
@@ -239,7 +254,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
       u.fused = false;
     }
   }
-  for (int qx = 0; qx < u.S[0]; ++qx)
+  for (int qx = 0; qx < (bf ? 0 : u.S[0]); ++qx)
     for (int qy = 0; qy < u.S[1]; ++qy)
       for (int qz = 0; qz < u.S[2]; ++qz) {
         const int Jx = cdiv(u.K[0] - qx, u.S[0]), Jy = cdiv(u.K[1] - qy, u.S[1]),
@@ -273,7 +288,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     a.KX = u.K[0]; a.KY = u.K[1]; a.KZ = u.K[2];
     a.sx = u.S[0]; a.sy = u.S[1]; a.sz = u.S[2];
     a.dx = a.dy = a.dz = 1;
-    if (int e = plan_conv_any(a, kTargetBlocks)) return e;
+    if (int e = bf ? plan_bconv(a, kTargetBlocks) : plan_conv_any(a, kTargetBlocks)) return e;
     u.dgrad = a;
     max_wprep = std::max(max_wprep, wprep_floats(a));
     max_part = std::max(max_part, (size_t)gconv_rows(a) * a.CoutW * 2);
@@ -291,7 +306,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     w.gdx = w.gdy = w.gdz = 1;
     w.taps_rows = 0;
     w.bias_row = 0;
-    if (int e = plan_wgrad(w, kTargetBlocks)) return e;
+    if (int e = bf ? plan_bwgrad(w, kTargetBlocks) : plan_wgrad(w, kTargetBlocks)) return e;
     u.wg = w;
     max_part = std::max(max_part, wgrad_partial_floats(w));
     max_part = std::max(max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
@@ -306,6 +321,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 struct hcu_unet_plan {
   hcu_unet_spec spec;
   int B, X, Y, Z, L;
+  int es = 4;          // activation element bytes: 4 (fp32 path) or 2 (bf16 path)
   Dims xin;
   size_t xcl_off = 0;
   std::vector<ConvLayer> dc1, dc2, uc1, uc2;
@@ -367,6 +383,11 @@ namespace {
 
 size_t prep_floats_fwd(const ConvLayer &L) { return wprep_floats(L.fwd); }
 size_t prep_floats_dgrad(const ConvLayer &L) { return wprep_floats(L.dgrad); }
+// Elements of a prepared weight image (bf16 images hold two per float slot).
+size_t prep_elems(const GConvArgs &a) {
+  if (a.use_bconv) return (size_t)wpack_count(wpack_of(a), a.KX * a.KY * a.KZ, a.ICs, a.CoutW);
+  return wprep_floats(a);
+}
 
 void track_conv(hcu_unet_plan &p, const ConvLayer &L) {
   p.max_act = std::max(p.max_act, std::max(L.in.floats(), L.out.floats()));
@@ -458,7 +479,10 @@ int build_plan(hcu_unet_plan &p) {
 
   // Shapes, forward order.
   Region saved;
-  p.xin = mkdims(p.B, p.X, p.Y, p.Z, s.in_channels);
+  if (s.compute_dtype != HCU_F32 && s.compute_dtype != HCU_BF16)
+    return fail(HCU_ERR_INVALID, "compute_dtype must be HCU_F32 or HCU_BF16");
+  p.es = s.compute_dtype == HCU_BF16 ? 2 : 4;
+  p.xin = mkdims(p.B, p.X, p.Y, p.Z, s.in_channels, p.es);
   p.xcl_off = saved.take_floats(p.xin.floats());
   p.max_act = p.xin.floats();
   Dims cur = p.xin;
@@ -476,7 +500,7 @@ int build_plan(hcu_unet_plan &p) {
       const int px = cur.X / s.pool_k[0], py = cur.Y / s.pool_k[1], pz = cur.Z / s.pool_k[2];
       if (px < 1 || py < 1 || pz < 1)
         return fail(HCU_ERR_SHAPE, "max_pool3d: Output size is too small");
-      p.pooled[i] = mkdims(p.B, px, py, pz, f);
+      p.pooled[i] = mkdims(p.B, px, py, pz, f, p.es);
       p.pool_off[i] = saved.take_floats(p.pooled[i].floats());
       p.max_act = std::max(p.max_act, p.pooled[i].floats());
       cur = p.pooled[i];
@@ -507,7 +531,7 @@ int build_plan(hcu_unet_plan &p) {
     cur = p.uc2[j].out;
   }
   if (p.Co > 4) return fail(HCU_ERR_UNSUPPORTED, "out_channels > 4 is not supported yet");
-  p.outd = mkdims(p.B, cur.X, cur.Y, cur.Z, p.Co);
+  p.outd = mkdims(p.B, cur.X, cur.Y, cur.Z, p.Co, 4);
   {
     const int R = outconv_bwd_rows(cur.vox(), cur.Cs);
     p.max_part = std::max(p.max_part, (size_t)R * cur.Cs * 2 + (size_t)R * (p.Co * cur.Cs + p.Co) + 64);
@@ -519,9 +543,10 @@ int build_plan(hcu_unet_plan &p) {
                      size_t &off) {
     PrepJob j{};
     j.kind = kind;
+    j.bf16 = p.es == 2;
     j.n = (int64_t)n;
     j.src = src;
-    off = saved.take_floats(n);
+    off = saved.take_floats(j.bf16 ? (n + 1) / 2 : n);
     j.dst = (int64_t)(off / sizeof(float));
     j.pk = pk;
     std::copy(prm, prm + np, j.p);
@@ -530,10 +555,10 @@ int build_plan(hcu_unet_plan &p) {
   auto conv_jobs = [&](ConvLayer &cl) {
     const int pf[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.fwd.ICs, cl.fwd.CoutW,
                        std::min(cl.fold_mod, cl.groups * cl.Cin_g)};
-    add_job(PREP_CONV_FWD, prep_floats_fwd(cl), cl.w_off, wpack_of(cl.fwd), pf, 8, cl.wf_off);
+    add_job(PREP_CONV_FWD, prep_elems(cl.fwd), cl.w_off, wpack_of(cl.fwd), pf, 8, cl.wf_off);
     const int pd[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.dgrad.ICs,
                        cl.dgrad.CoutW, cl.E};
-    add_job(PREP_CONV_DGRAD, prep_floats_dgrad(cl), cl.w_off, wpack_of(cl.dgrad), pd, 8,
+    add_job(PREP_CONV_DGRAD, prep_elems(cl.dgrad), cl.w_off, wpack_of(cl.dgrad), pd, 8,
             cl.wd_off);
   };
   for (int i = 0; i < L; ++i) {
@@ -547,7 +572,7 @@ int build_plan(hcu_unet_plan &p) {
     if (u.fused) {
       const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
                           u.fwdf.ICs, u.fwdf.CoutW};
-      add_job(PREP_CONVT_FUSED, wprep_floats(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 10, u.wf_off);
+      add_job(PREP_CONVT_FUSED, prep_elems(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 10, u.wf_off);
     } else {
       u.wph_off.assign(u.phases.size(), 0);
       for (size_t ph = 0; ph < u.phases.size(); ++ph) {
@@ -560,7 +585,7 @@ int build_plan(hcu_unet_plan &p) {
       }
     }
     const int pd[5] = {u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW};
-    add_job(PREP_CONVT_DGRAD, wprep_floats(u.dgrad), u.w_off, wpack_of(u.dgrad), pd, 5, u.wd_off);
+    add_job(PREP_CONVT_DGRAD, prep_elems(u.dgrad), u.w_off, wpack_of(u.dgrad), pd, 5, u.wd_off);
   }
   p.saved_bytes = saved.off;
 
@@ -590,6 +615,7 @@ struct Ctx {
   int next_slot = 0;
   unsigned slot_read = 0;   // slots whose last reader event was recorded in this enqueue
   float *fptr(char *base, size_t off) const { return reinterpret_cast<float *>(base + off); }
+  int bf() const { return p.es == 2; }   // bf16 activation storage
   float *part() const { return fptr(sc, p.part_off); }
   float *wpart() const { return fptr(sc, split ? p.wpart_off : p.part_off); }
   float *wprep() const { return fptr(sc, p.wprep_off); }
@@ -675,7 +701,8 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
                                      bnl.bn.count, coef, c.G + bnl.bn.gamma, c.G + bnl.bn.beta,
                                      training, accumulate, c.s))
     return e;
-  return launch_bn_bwd_apply(dz, c.fptr(c.sv, bnl.y_off), coef, bnl.out.vox(), bnl.out.Cs, c.s);
+  return launch_bn_bwd_apply(dz, c.fptr(c.sv, bnl.y_off), coef, bnl.out.vox(), bnl.out.Cs, c.s,
+                             c.bf());
 }
 
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
@@ -739,16 +766,17 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
   if (pool_dP) {
     if (int e = launch_bn_bwd_reduce_pool(pool_dP, y, coef, dbuf, L.out.B, L.out.X, L.out.Y,
                                           L.out.Z, L.out.Cs, pool_k[0], pool_k[1], pool_k[2],
-                                          c.part(), R, c.s))
+                                          c.part(), R, c.s, c.bf()))
       return e;
   } else {
-    if (int e = launch_bn_bwd_reduce_dense(dbuf, y, coef, nvox, L.out.Cs, c.part(), R, c.s))
+    if (int e = launch_bn_bwd_reduce_dense(dbuf, y, coef, nvox, L.out.Cs, c.part(), R, c.s,
+                                           c.bf()))
       return e;
   }
   if (int e = launch_bn_bwd_finalize(c.part(), R, L.bn.C, L.bn.Cs, L.bn.Cs, L.bn.count, coef,
                                      c.G + L.bn.gamma, c.G + L.bn.beta, training, accumulate, c.s))
     return e;
-  return launch_bn_bwd_apply(dbuf, y, coef, nvox, L.out.Cs, c.s);
+  return launch_bn_bwd_apply(dbuf, y, coef, nvox, L.out.Cs, c.s, c.bf());
 }
 
 }  // namespace
@@ -883,7 +911,7 @@ int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int 
     r.Z = L.out.Z;
     r.C = L.out.C;
     r.Cs = L.out.Cs;
-    r.elem_bytes = 4;
+    r.elem_bytes = L.out.es;
     out[i] = r;
   }
   return p->n_bn;
@@ -895,7 +923,9 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
   tag(std::string("in"), "fwd");
-  if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
+  if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
+                           t->x_dtype))
+    return e;
   tag(std::string("prep"), "fwd");
   if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_jobs.data(),
                               (int)p.prep_jobs.size(), c.s))
@@ -913,7 +943,7 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
       tag(c2.name, "pool");
       if (int e = launch_maxpool_fwd(c.fptr(c.sv, c2.y_off), b2.scale, b2.shift, pp, p.B,
                                      c2.out.X, c2.out.Y, c2.out.Z, c2.out.Cs, s.pool_k[0],
-                                     s.pool_k[1], s.pool_k[2], c.s))
+                                     s.pool_k[1], s.pool_k[2], c.s, c.bf()))
         return e;
       src = pp;
       ssc = ssh = nullptr;
@@ -962,7 +992,8 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   const ConvLayer &last = p.L > 1 ? p.uc2[p.L - 2] : p.dc2[0];
   tag(std::string("out"), "fwd");
   if (int e = launch_outconv_fwd(src, coef_at(c.sv, last.bn), c.P + p.oc_w, c.P + p.oc_b, t->out,
-                                 p.B, last.out.vox() / p.B, last.out.C, last.out.Cs, p.Co, c.s))
+                                 p.B, last.out.vox() / p.B, last.out.C, last.out.Cs, p.Co, c.s,
+                                 c.bf()))
     return e;
   if (training && t->bn_num_batches_tracked)
     if (int e = launch_bn_count_increment(t->bn_num_batches_tracked, p.n_bn, c.s)) return e;
@@ -975,6 +1006,9 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   if (!plan || !t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
     return fail(HCU_ERR_INVALID, "null argument");
   const hcu_unet_plan &p = *plan;
+  if (t->x_dtype != HCU_F32 && t->x_dtype != HCU_F16 &&
+      !(t->x_dtype == HCU_BF16 && p.es == 2))
+    return fail(HCU_ERR_INVALID, "unsupported input dtype for this plan");
   if (training) {
     for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
       for (const ConvLayer &L : *v)
@@ -982,7 +1016,8 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
           return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
   }
   std::vector<uintptr_t> key = {0, (uintptr_t)t->x, (uintptr_t)t->out, (uintptr_t)t->params,
-                                (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)training};
+                                (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)training,
+                                (uintptr_t)t->x_dtype};
   append_bn_key(key, p, t);
   return run_graphed(p, key, (hipStream_t)stream,
                      [&](hipStream_t s) { return enqueue_forward(p, t, training, s); });
@@ -1009,7 +1044,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     float *part_oc = part_bn + (size_t)R * last.out.Cs * 2;
     if (int e = launch_outconv_bwd(dout, c.fptr(c.sv, last.y_off), coef, c.P + p.oc_w, c.buf(cur),
                                    p.B, nvox / p.B, last.out.C, last.out.Cs, p.Co, part_bn, part_oc,
-                                   R, c.s))
+                                   R, c.s, c.bf()))
       return e;
     if (int e = launch_outconv_wfinalize(part_oc, R, p.Co, last.out.C, last.out.Cs, c.G + p.oc_w,
                                          c.G + p.oc_b, accumulate, c.s))
@@ -1019,7 +1054,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
                                        accumulate, c.s))
       return e;
     if (int e = launch_bn_bwd_apply(c.buf(cur), c.fptr(c.sv, last.y_off), coef, nvox,
-                                    last.out.Cs, c.s))
+                                    last.out.Cs, c.s, c.bf()))
       return e;
   }
   // decoder, last to first
@@ -1049,7 +1084,8 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.fork()) return e;
     {
       const int R = chansum_rows(u.out.vox(), u.out.Cs);
-      if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, c.wpart(), R, c.wstream())) return e;
+      if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, c.wpart(), R, c.wstream(), c.bf()))
+        return e;
       if (int e = launch_reduce_partials(c.wpart(), R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate,
                                          c.wstream()))
         return e;
@@ -1126,7 +1162,8 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
         return e;
       cur = sp;
     } else if (dx) {
-      if (int e = launch_from_cl(dIn, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s)) return e;
+      if (int e = launch_from_cl(dIn, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf()))
+        return e;
     }
   }
   if (int e = c.join()) return e;
@@ -1194,7 +1231,8 @@ struct OpPlan {
 
 int make_op(const hcu_conv_desc *d, OpPlan &op) {
   if (!d) return fail(HCU_ERR_INVALID, "null descriptor");
-  const Dims in = mkdims(d->B, d->X, d->Y, d->Z, d->Cin);
+  if (d->dtype != HCU_F32 && d->dtype != HCU_BF16) return fail(HCU_ERR_INVALID, "bad dtype");
+  const Dims in = mkdims(d->B, d->X, d->Y, d->Z, d->Cin, d->dtype == HCU_BF16 ? 2 : 4);
   if (!d->transposed) {
     for (int i = 0; i < 3; ++i)
       if (d->stride[i] != 1) return fail(HCU_ERR_UNSUPPORTED, "Conv3d: only stride 1 (valid) is supported");
@@ -1217,6 +1255,20 @@ int make_op(const hcu_conv_desc *d, OpPlan &op) {
   op.kpart_off = r.take_floats(std::max<size_t>(op.max_kpart, 1));
   op.scratch_bytes = r.off;
   return 0;
+}
+
+// One weight re-layout through the batched prep kernel (the bf16 images).
+int prep_one(int kind, const GConvArgs &a, const int *prm, int np, const float *w, float *dst,
+             hipStream_t s) {
+  PrepJob j{};
+  j.kind = kind;
+  j.bf16 = a.use_bconv ? 1 : 0;
+  j.n = (int64_t)prep_elems(a);
+  j.src = 0;
+  j.dst = 0;
+  j.pk = wpack_of(a);
+  std::copy(prm, prm + np, j.p);
+  return launch_prep_all(w, dst, &j, 1, s);
 }
 
 int check_scratch(const OpPlan &op, void *scratch, size_t bytes) {
@@ -1255,9 +1307,14 @@ int hcu_conv_fwd_cl(const hcu_conv_desc *d, const float *x, const float *w, cons
   float *kpart = reinterpret_cast<float *>((char *)scratch + op.kpart_off);
   if (!d->transposed) {
     const ConvLayer &L = op.conv;
-    if (int e = launch_prep_conv_fwd(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
-                                     L.fwd.ICs, L.fwd.CoutW, wpack_of(L.fwd), s))
+    if (L.fwd.use_bconv) {
+      const int pf[8] = {L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T, L.fwd.ICs, L.fwd.CoutW,
+                         std::min(L.fold_mod, L.groups * L.Cin_g)};
+      if (int e = prep_one(PREP_CONV_FWD, L.fwd, pf, 8, w, wprep, s)) return e;
+    } else if (int e = launch_prep_conv_fwd(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
+                                            L.fwd.ICs, L.fwd.CoutW, wpack_of(L.fwd), s)) {
       return e;
+    }
     GConvArgs a = L.fwd;
     a.in = x;
     a.w = wprep;
@@ -1269,9 +1326,15 @@ int hcu_conv_fwd_cl(const hcu_conv_desc *d, const float *x, const float *w, cons
   const ConvTLayer &u = op.ct;
   if (u.fused) {
     GConvArgs a = u.fwdf;
-    if (int e = launch_prep_convt_fused(w, wprep, u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0],
-                                        u.S[1], u.S[2], a.ICs, a.CoutW, wpack_of(a), s))
+    if (a.use_bconv) {
+      const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2], a.ICs,
+                          a.CoutW};
+      if (int e = prep_one(PREP_CONVT_FUSED, a, pf, 10, w, wprep, s)) return e;
+    } else if (int e = launch_prep_convt_fused(w, wprep, u.Cin, u.Cout, u.K[0], u.K[1], u.K[2],
+                                               u.S[0], u.S[1], u.S[2], a.ICs, a.CoutW,
+                                               wpack_of(a), s)) {
       return e;
+    }
     a.in = x;
     a.w = wprep;
     a.bias = bias;
@@ -1306,15 +1369,25 @@ int hcu_conv_dgrad_cl(const hcu_conv_desc *d, const float *dy, const float *w, f
   GConvArgs a;
   if (!d->transposed) {
     const ConvLayer &L = op.conv;
-    if (int e = launch_prep_conv_dgrad(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T,
-                                       L.dgrad.ICs, L.dgrad.CoutW, L.E, wpack_of(L.dgrad), s))
+    if (L.dgrad.use_bconv) {
+      const int pd[8] = {L.Cout, L.Cin_g, L.groups, L.fold_mod, L.T, L.dgrad.ICs, L.dgrad.CoutW,
+                         L.E};
+      if (int e = prep_one(PREP_CONV_DGRAD, L.dgrad, pd, 8, w, wprep, s)) return e;
+    } else if (int e = launch_prep_conv_dgrad(w, wprep, L.Cout, L.Cin_g, L.groups, L.fold_mod,
+                                              L.T, L.dgrad.ICs, L.dgrad.CoutW, L.E,
+                                              wpack_of(L.dgrad), s)) {
       return e;
+    }
     a = L.dgrad;
   } else {
     const ConvTLayer &u = op.ct;
-    if (int e = launch_prep_convt_dgrad(w, wprep, u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW,
-                                        wpack_of(u.dgrad), s))
+    if (u.dgrad.use_bconv) {
+      const int pd[5] = {u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW};
+      if (int e = prep_one(PREP_CONVT_DGRAD, u.dgrad, pd, 5, w, wprep, s)) return e;
+    } else if (int e = launch_prep_convt_dgrad(w, wprep, u.Cin, u.Cout, u.T, u.dgrad.ICs,
+                                               u.dgrad.CoutW, wpack_of(u.dgrad), s)) {
       return e;
+    }
     a = u.dgrad;
   }
   a.in = dy;
@@ -1366,7 +1439,7 @@ int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy, f
   if (d->transposed && dbias) {
     const ConvTLayer &u = op.ct;
     const int R = chansum_rows(u.out.vox(), u.out.Cs);
-    if (int e = launch_chansum(dy, u.out.vox(), u.out.Cs, part, R, s)) return e;
+    if (int e = launch_chansum(dy, u.out.vox(), u.out.Cs, part, R, s, u.out.es == 2)) return e;
     if (int e = launch_reduce_partials(part, R, u.out.Cs, u.Cout, dbias, 0, s)) return e;
   }
   return HCU_OK;

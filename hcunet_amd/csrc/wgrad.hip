@@ -628,6 +628,7 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
 }
 
 int launch_wgrad(const WGradArgs &a, hipStream_t s) {
+  if (a.use_bw) return launch_bwgrad(a, s);
   const dim3 grid(a.KB, a.mchunks, a.nchunks);
   const int T = a.KX * a.KY * a.KZ;
   if (a.v2) {

@@ -12,7 +12,15 @@ Interface parity with the reference (hcat/unet.py):
 Compute: forward/backward of the whole network are ONE autograd node whose
 forward and backward are single calls into the native executor
 (hcu_unet_forward / hcu_unet_backward), which enqueue the HIP kernels on the
-current stream.  Parameters live in one flat fp32 buffer (each nn.Parameter is
+current stream.
+
+Precision: by default the network computes in fp32, exactly the reference's
+arithmetic.  Under torch.autocast('cuda', dtype=torch.bfloat16) (or with
+`module.compute_dtype = torch.bfloat16`) it runs the bf16 path of BASELINE
+config 3: bf16 activations, gradients and MFMA operands, fp32 accumulation,
+BatchNorm statistics, parameters and optimizer state; the input may then be a
+fp32, fp16 or bf16 volume (16-bit volumes are read directly by the first
+kernel), and the logits are returned in fp32.  Parameters live in one flat fp32 buffer (each nn.Parameter is
 a view of it) and gradients are written into one flat buffer whose views are
 attached as .grad, so the optimizer step and the data-parallel all-reduce are
 single launches over contiguous memory.
@@ -99,6 +107,8 @@ class Unet_Constructor(nn.Module):
         self.up_steps = nn.ModuleList(up)
         self.max_pool = conv_functions[2](max_pool_kernel)
         self._engine = None
+        # None: follow torch.autocast; torch.float32 / torch.bfloat16: force
+        self.compute_dtype = None
 
     # -- nn.Module plumbing ------------------------------------------------
     def _apply(self, fn, *args, **kwargs):
@@ -111,14 +121,24 @@ class Unet_Constructor(nn.Module):
             self._engine = _Engine(self)
         return self._engine
 
+    def _bf16(self):
+        cd = getattr(self, 'compute_dtype', None)
+        if cd is not None:
+            if cd not in (torch.float32, torch.bfloat16):
+                raise ValueError('compute_dtype must be torch.float32 or torch.bfloat16')
+            return cd == torch.bfloat16
+        return bool(torch.is_autocast_enabled('cuda')
+                    and torch.get_autocast_dtype('cuda') == torch.bfloat16)
+
     def forward(self, x):
         if not isinstance(x, torch.Tensor):
             raise TypeError(f'Expected input of type torch.Tensor, not {type(x)}')
         _lib.require_device(x, 'Unet_Constructor input')
         eng = self.engine()
-        eng.check_input(x)
+        bf16 = self._bf16()
+        eng.check_input(x, bf16)
         params = eng.params_ready()
-        return _UnetFunction.apply(x, eng, *params)
+        return _UnetFunction.apply(x, eng, bf16, *params)
 
     # -- checkpointing (hcat/unet.py:145-196) --------------------------------
     def save(self, filename, hyperparameters=None):
@@ -352,7 +372,7 @@ class _Engine:
         self.params = None
         self._bn_arrays = None
 
-    def check_input(self, x):
+    def check_input(self, x, bf16=False):
         m = self.module_ref
         if x.dim() != 5:
             raise RuntimeError('Expected 5D input [B, C, X, Y, Z] for conv3d, got %dD' % x.dim())
@@ -361,15 +381,18 @@ class _Engine:
             raise RuntimeError('Given groups=%d, expected input%s to have %d channels, but got %d '
                                'channels instead' % (m.down_steps[0].conv1.groups,
                                                      list(x.shape), cin, x.shape[1]))
-        if x.dtype != torch.float32:
+        ok = (torch.float32, torch.float16, torch.bfloat16) if bf16 else (torch.float32,)
+        if x.dtype not in ok:
             raise RuntimeError('Input type (%s) and weight type (float) should be the same' % x.dtype)
 
-    def plan(self, shape):
-        key = tuple(shape)
+    def plan(self, shape, bf16=False):
+        key = tuple(shape) + (bool(bf16),)
         p = self.plans.get(key)
         if p is None:
-            B, _, X, Y, Z = key
-            p = _Plan(self.spec, B, X, Y, Z)
+            B, _, X, Y, Z = tuple(shape)
+            spec = _lib.UnetSpec.from_buffer_copy(self.spec)
+            spec.compute_dtype = _lib.HCU_BF16 if bf16 else _lib.HCU_F32
+            p = _Plan(spec, B, X, Y, Z)
             self.plans[key] = p
         return p
 
@@ -444,6 +467,7 @@ class _Engine:
         t.bn_num_batches_tracked = ctypes.cast(nb, ctypes.POINTER(ctypes.c_void_p))
         t.saved = saved.data_ptr()
         t.scratch = scratch.data_ptr()
+        t.x_dtype = _X_DTYPES[x.dtype]
         return t
 
     def grad_target(self):
@@ -489,13 +513,15 @@ class _Engine:
 
 
 _POISON = os.environ.get('HCU_POISON') == '1'
+_X_DTYPES = {torch.float32: _lib.HCU_F32, torch.float16: _lib.HCU_F16,
+             torch.bfloat16: _lib.HCU_BF16}
 
 
 class _UnetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, eng, *params):
+    def forward(ctx, x, eng, bf16, *params):
         x = x.contiguous()
-        plan = eng.plan(x.shape)
+        plan = eng.plan(x.shape, bf16)
         dev = x.device
         out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
         saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
@@ -529,7 +555,7 @@ class _UnetFunction(torch.autograd.Function):
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
         if _POISON:
             scratch.fill_(255)
-        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dx = torch.empty(x.shape, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
         G, accumulate, finish = eng.grad_target()
         t = eng.tensors(x, None, saved, scratch, grads=G)
         with torch.cuda.device(dev):
@@ -539,4 +565,6 @@ class _UnetFunction(torch.autograd.Function):
                                                     _lib.stream_handle(dev)),
                        'Unet_Constructor.backward')
         finish()
-        return (dx, None) + (None,) * len(eng.params)
+        if dx is not None and dx.dtype != x.dtype:
+            dx = dx.to(x.dtype)
+        return (dx, None, None) + (None,) * len(eng.params)

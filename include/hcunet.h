@@ -57,7 +57,7 @@ enum {
   HCU_ERR_WORKSPACE = 5    /* workspace too small */
 };
 
-enum { HCU_F32 = 0, HCU_F16 = 1, HCU_U8 = 2 };
+enum { HCU_F32 = 0, HCU_F16 = 1, HCU_U8 = 2, HCU_BF16 = 3 };
 
 const char *hcu_last_error(void);
 int hcu_version(void);
@@ -82,6 +82,11 @@ typedef struct hcu_unet_spec {
   int pool_k[3];                    /* max_pool_kernel (kernel = stride)    */
   float bn_eps;                     /* BatchNorm3d eps (1e-5)               */
   float bn_momentum;                /* 0.1; < 0 means momentum=None         */
+  int compute_dtype;                /* HCU_F32: fp32 throughout (the reference's
+                                       arithmetic); HCU_BF16: bf16 activations,
+                                       gradients and GEMM operands, fp32
+                                       accumulation / statistics / parameters
+                                       (torch.autocast(dtype=torch.bfloat16)) */
 } hcu_unet_spec;
 
 typedef struct hcu_unet_plan hcu_unet_plan;
@@ -103,7 +108,7 @@ int hcu_unet_plan_query(const hcu_unet_plan *plan, int64_t *out_shape,
                         size_t *scratch_bytes);
 
 typedef struct hcu_unet_tensors {
-  const float *x;          /* [B][Cin][X][Y][Z] fp32                         */
+  const float *x;          /* [B][Cin][X][Y][Z] of x_dtype (fp32 by default) */
   float *out;              /* [B][Cout][OX][OY][OZ] fp32                     */
   const float *params;     /* flat fp32, Unet_Constructor.parameters() order */
   float *grads;            /* flat fp32, same layout (backward only)         */
@@ -112,6 +117,9 @@ typedef struct hcu_unet_tensors {
   int64_t *const *bn_num_batches_tracked;
   void *saved;             /* saved_bytes   */
   void *scratch;           /* scratch_bytes */
+  int x_dtype;             /* HCU_F32, or with compute_dtype HCU_BF16 also
+                              HCU_F16 / HCU_BF16 (16-bit volumes are read
+                              directly by the channels-last staging kernel) */
 } hcu_unet_tensors;
 
 /* training != 0: BatchNorm uses batch statistics and updates running stats
@@ -182,6 +190,9 @@ typedef struct hcu_conv_desc {
   int groups;              /* Conv3d only                                     */
   int transposed;          /* 0: nn.Conv3d (valid, stride 1 only)
                               1: nn.ConvTranspose3d (pad 0, dil 1, groups 1) */
+  int dtype;               /* HCU_F32: fp32 activations, Cs = round_up(C, 4);
+                              HCU_BF16: bf16 activations (x, y, dy, dx),
+                              Cs = round_up(C, 8); weights / dw / bias fp32 */
 } hcu_conv_desc;
 
 size_t hcu_conv_scratch_bytes(const hcu_conv_desc *d);

@@ -34,9 +34,12 @@ def main():
     opt = hcunet_amd.optim.Adam(m.parameters(), lr=1e-3)
     x, mask, pwl = bench.synth_inputs(cfg['batch'], 1000, dev)
 
+    bf16 = cfg.get('dtype') == 'bf16'
+
     def step():
         opt.zero_grad()
-        loss = cross_entropy(m(x), mask, pwl, method='pixel')
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=bf16):
+            loss = cross_entropy(m(x), mask, pwl, method='pixel')
         loss.backward()
         opt.step()
     for _ in range(3):
