@@ -41,7 +41,12 @@
 namespace hcu {
 
 namespace {
-constexpr int ckp_of(int CK) { return CK == 8 ? 8 : CK + 8; }
+// Halo row stride (bf16 elements).  ds_read_b128 serves a wave in 4 lane
+// groups of 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...); with CK = 32 the
+// lanes of one group read rows r of chunk g and rows r' of chunk g+1, and a
+// row of 6 x 16-byte slots (CK + 16) puts all 16 on distinct bank slots for
+// consecutive rows; CK = 16 uses 3 slots, CK = 8 one (rows are contiguous).
+constexpr int ckp_of(int CK) { return CK == 8 ? 8 : (CK == 16 ? 24 : CK + 16); }
 }
 
 template <int CK, int NSUB, int MPW, int NPF>
@@ -63,6 +68,11 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   int *toffs = reinterpret_cast<int *>(wlds + S * 4 * NT * 8);    // [S][4]
   int *rowpk = toffs + S * 4;                                     // [MPW*64]
   int *rowoff = rowpk + MPW * 64;                                 // [MPW*64]
+  // per-block coefficients live in LDS, not registers (they are only needed in
+  // short phases): epilogue [6][NT] = bias, bn scale/shift/mean/invstd, stats
+  // pivot per stored column; input activation [2][ICs] = scale, shift
+  float *coefL = reinterpret_cast<float *>(rowoff + MPW * 64);
+  float *actL = coefL + 6 * NT;
 
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
@@ -109,6 +119,28 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     toffs[e] = off * CKP + ((e & 3) % C8) * 8;
   }
 
+  {
+    int ph0 = 0, c00 = n0;
+    if (a.nph > 1) {
+      ph0 = n0 / a.Cout;
+      c00 = n0 - ph0 * a.Cout;
+    }
+    for (int j = tid; j < NT; j += 256) {
+      const int c = c00 + j;
+      coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
+      const bool bn = a.bn_y && !split && c < a.OCs;
+      coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;
+      coefL[2 * NT + j] = bn ? a.bn_shift[c] : 0.f;
+      coefL[3 * NT + j] = bn ? a.bn_mean[c] : 0.f;
+      coefL[4 * NT + j] = bn ? a.bn_invstd[c] : 0.f;
+      coefL[5 * NT + j] = 0.f;
+    }
+    if (a.in_scale)
+      for (int c = tid; c < a.ICs; c += 256) {
+        actL[c] = a.in_scale[c];
+        actL[a.ICs + c] = a.in_shift[c];
+      }
+  }
   auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
     int r, tzi, tyi, txi;
     a.fNT.divmod(tile, b, r);
@@ -177,26 +209,22 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
   };
   // BatchNorm+ReLU of 8 channels (fp32), 0 outside the input
-  auto activate = [&](uint4 v, bool ok, const float (&sc)[8], const float (&sh)[8]) -> uint4 {
+  // BatchNorm+ReLU of 8 channels (fp32; coefficients from LDS), 0 outside the input
+  auto activate = [&](uint4 v, bool ok, int chunk) -> uint4 {
     if (!ok) return make_uint4(0u, 0u, 0u, 0u);
     if (!act) return v;
+    const int c = chunk * CK + c8 * 8;
+    const float4 s0 = *reinterpret_cast<const float4 *>(actL + c);
+    const float4 s1 = *reinterpret_cast<const float4 *>(actL + c + 4);
+    const float4 h0 = *reinterpret_cast<const float4 *>(actL + a.ICs + c);
+    const float4 h1 = *reinterpret_cast<const float4 *>(actL + a.ICs + c + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     float f[8];
     unpack8(v, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
     return pack8(f);
-  };
-  auto load_act = [&](int chunk, float (&sc)[8], float (&sh)[8]) {
-    if (!act) return;
-    const int c = chunk * CK + c8 * 8;
-    const float4 s0 = *reinterpret_cast<const float4 *>(a.in_scale + c);
-    const float4 s1 = *reinterpret_cast<const float4 *>(a.in_scale + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4 *>(a.in_shift + c);
-    const float4 h1 = *reinterpret_cast<const float4 *>(a.in_shift + c + 4);
-    sc[0] = s0.x; sc[1] = s0.y; sc[2] = s0.z; sc[3] = s0.w;
-    sc[4] = s1.x; sc[5] = s1.y; sc[6] = s1.z; sc[7] = s1.w;
-    sh[0] = h0.x; sh[1] = h0.y; sh[2] = h0.z; sh[3] = h0.w;
-    sh[4] = h1.x; sh[5] = h1.y; sh[6] = h1.z; sh[7] = h1.w;
   };
   // direct (non-prefetched) staging of one (tile, chunk) halo
   auto stage_direct = [&](int tile, int chunk) {
@@ -206,8 +234,6 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     const uint16_t *bp = reinterpret_cast<const uint16_t *>(a.in) + (size_t)b * a.IX * a.IY * a.IZ * a.ICs;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, sample_bytes, 0x00020000);
-    float sc[8], sh[8];
-    load_act(chunk, sc, sh);
     for (int base = tid / C8; base < HV; base += 4 * VS) {
       uint4 val[4];
       bool okv[4];
@@ -229,7 +255,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       for (int u = 0; u < 4; ++u) {
         const int v = base + u * VS;
         if (v < HV)
-          *reinterpret_cast<uint4 *>(alds + v * CKP + c8 * 8) = activate(val[u], okv[u], sc, sh);
+          *reinterpret_cast<uint4 *>(alds + v * CKP + c8 * 8) = activate(val[u], okv[u], chunk);
       }
     }
   };
@@ -279,24 +305,18 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   const int qz = ph % a.phz, qy = (ph / a.phz) % a.phy, qx = ph / (a.phz * a.phy);
   const int cst = co0 + ec8 * 8;         // first stored channel of this thread
   const bool cok = cst < a.OCs;
-  float bias8[8], bsc[8], bsh[8], bmu[8], bis[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = cst + k;
-    bias8[k] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
-    bsc[k] = bsh[k] = bmu[k] = bis[k] = 0.f;
-    if (a.bn_y && !split && c < a.OCs) {
-      bsc[k] = a.bn_scale[c];
-      bsh[k] = a.bn_shift[c];
-      bmu[k] = a.bn_mean[c];
-      bis[k] = a.bn_invstd[c];
-    }
-  }
   const bool fwdstat = a.stats && !a.bn_y && !split;
-  float st1[8], st2[8], piv[8], cnt = 0.f;
+  float st1[8], st2[8], cnt = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) st1[k] = st2[k] = piv[k] = 0.f;
+  for (int k = 0; k < 8; ++k) st1[k] = st2[k] = 0.f;
   bool have_piv = false;
+  // 8 consecutive LDS floats of coefficient array q for this thread's channels
+  auto coef8 = [&](int q, float (&o)[8]) {
+    const float4 c0 = *reinterpret_cast<const float4 *>(coefL + q * NT + ec8 * 8);
+    const float4 c1 = *reinterpret_cast<const float4 *>(coefL + q * NT + ec8 * 8 + 4);
+    o[0] = c0.x; o[1] = c0.y; o[2] = c0.z; o[3] = c0.w;
+    o[4] = c1.x; o[5] = c1.y; o[6] = c1.z; o[7] = c1.w;
+  };
   float *dstf = split ? a.partial + (size_t)blockIdx.z * a.slice_floats : nullptr;
   uint16_t *dsth = reinterpret_cast<uint16_t *>(a.out);
   const uint16_t *ybf = reinterpret_cast<const uint16_t *>(a.bn_y);
@@ -314,10 +334,17 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       }
     }
     __syncthreads();
+    float bias8[8], piv[8];
+    coef8(0, bias8);
     if (fwdstat && !have_piv) {   // pivot: the block's first output voxel (row 0)
 #pragma unroll
       for (int k = 0; k < 8; ++k) piv[k] = smem[ec8 * 8 + k] + bias8[k];
+      if (tid < nc8)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) coefL[5 * NT + ec8 * 8 + k] = piv[k];
       have_piv = true;
+    } else {
+      coef8(5, piv);
     }
     const size_t tbase =
         ((((size_t)b * a.SX + ox0 * a.osx + a.ofx + qx) * a.SY + oy0 * a.osy + a.ofy + qy) * a.SZ +
@@ -344,7 +371,11 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] += bias8[k];
       if (a.bn_y) {   // fused BatchNorm+ReLU backward: v = dA -> dz; (dz, dz*xhat)
-        float y[8];
+        float y[8], bsc[8], bsh[8], bmu[8], bis[8];
+        coef8(1, bsc);
+        coef8(2, bsh);
+        coef8(3, bmu);
+        coef8(4, bis);
         unpack8(*reinterpret_cast<const uint4 *>(ybf + off), y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -366,32 +397,34 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   };
 
   // ---- main loop over (tile, chunk) items
+  // contiguous tile range per block: consecutive tiles share halo rows, which
+  // then come from this CU's L1/L2 instead of HBM
+  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
   if (NPF > 0) {
-    int tile = blockIdx.x;
-    if (tile < total) fetch(tile, cb);
+    int tile = t_beg;
+    if (tile < t_end) fetch(tile, cb);
     if (nck == 1) stage_w(cb);
-    float sc[8], sh[8];
-    for (; tile < total; tile += gridDim.x) {
+    for (; tile < t_end; ++tile) {
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
 #pragma unroll
         for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
-        load_act(chunk, sc, sh);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < NPFR; ++u)
           if (hpk[u] >= 0)
             *reinterpret_cast<uint4 *>(alds + (tid / C8 + u * VS) * CKP + c8 * 8) =
-                activate(pf[u], (okbits >> u) & 1u, sc, sh);
+                activate(pf[u], (okbits >> u) & 1u, chunk);
         if (nck > 1) stage_w(chunk);
         __syncthreads();
         int nt = tile, nc = chunk + 1;
         if (nc == ce) {
           nc = cb;
-          nt = tile + gridDim.x;
+          nt = tile + 1;
         }
-        if (nt < total) fetch(nt, nc);
+        if (nt < t_end) fetch(nt, nc);
         compute();
       }
       int b, ox0, oy0, oz0;
@@ -399,7 +432,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       epilogue(b, ox0, oy0, oz0);
     }
   } else {
-    for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    for (int tile = t_beg; tile < t_end; ++tile) {
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
 #pragma unroll
@@ -437,7 +470,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       const size_t row = blockIdx.x;
       if (fwdstat)
         *reinterpret_cast<float4 *>(a.stats + (row * a.CoutW + c) * 4) =
-            make_float4(t1, t2, piv[k], tn);
+            make_float4(t1, t2, coefL[5 * NT + tid * 8 + k], tn);
       else {
         a.stats[(row * a.CoutW + c) * 2 + 0] = t1;
         a.stats[(row * a.CoutW + c) * 2 + 1] = t2;
@@ -565,7 +598,8 @@ static long bconv_lds(const GConvArgs &a, int CK, int NT) {
   const int T = a.KX * a.KY * a.KZ;
   const int TPS = 32 / CK;
   const int S = (T + TPS - 1) / TPS;
-  return std::max(bconv_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128,
+  return std::max(bconv_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128 +
+                      6L * NT + 2L * a.ICs,
                   256L * 3) * 4;
 }
 
@@ -588,56 +622,87 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   if (a.phx < 1) a.phx = 1;
   if (a.phy < 1) a.phy = 1;
   if (a.phz < 1) a.phz = 1;
+  const int T = a.KX * a.KY * a.KZ;
   const int Nlog = a.Cout * a.nph;
   const int nb16 = cdiv(Nlog, 16);
-  a.NSUB = nb16 >= 4 ? 4 : (nb16 >= 2 ? 2 : 1);
-  if (a.nph > 1) {   // a column block never straddles two stride phases
-    while (a.NSUB > 1 && a.Cout % (a.NSUB * 16)) a.NSUB /= 2;
-    if (a.Cout % (a.NSUB * 16) || a.Cout % 8)
-      return fail(4, "bconv: ConvTranspose3d with out_channels % 16 != 0 is not supported in bf16");
-  }
-  const int NT = a.NSUB * 16;
-  a.CoutW = round_up(Nlog, NT);
   const int ntz = cdiv(a.OZ, 16);
   a.TZ = cdiv(a.OZ, ntz);
-  const int nN = a.CoutW / NT;
-  const int mpw_target = env_int_b("HCU_BCONV_MPW_TARGET", 512);
-  const int mpws[3] = {4, 2, 1};
-  bool enough = false;
-  a.CK = 0;
-  for (int mi = 0; mi < 3 && !(enough && a.CK); ++mi) {
-    const int MPW = mpws[mi];
-    int TX, TY;
-    btile(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
-    const long blocks = (long)cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz * nN * a.B;
-    a.MPW = MPW;
-    a.TX = TX;
-    a.TY = TY;
-    a.HX = (a.TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
-    a.HY = (a.TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
-    a.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
-    enough = blocks >= mpw_target;
-    a.CK = 0;
-    const int cks[3] = {32, 16, 8};
-    for (int i = 0; i < 3; ++i) {
-      const int CK = cks[i];
-      if (a.ICs % CK) continue;
-      const long lds = bconv_lds(a, CK, NT);
-      if (lds <= 64 * 1024) {
-        a.CK = CK;
-        a.lds_bytes = (int)lds;
-        break;
+  const long lds_cap = env_int_b("HCU_BCONV_LDS_KB", 80) * 1024L;
+  // Candidate tilings, scored by a simple per-CU time model (cycles):
+  //   per (tile, chunk): MFMA S * MPW * NSUB * 16 per wave, staging ~
+  //   1200 + 40 per 16-byte element per thread (+ weights when multi-chunk);
+  //   per tile: epilogue ~1500; two resident blocks hide ~40 % of a block's
+  //   staging behind the other's MFMAs.
+  double best = 1e300;
+  GConvArgs bestA = a;
+  bool found = false;
+  const int mpws[3] = {4, 2, 1}, nsubs[3] = {4, 2, 1}, cks[3] = {32, 16, 8};
+  for (int ni = 0; ni < 3; ++ni) {
+    const int NSUB = nsubs[ni];
+    if (NSUB > 1 && nb16 < NSUB && !(NSUB == 2 && nb16 >= 2)) continue;
+    if (NSUB == 4 && nb16 < 4) continue;
+    if (NSUB == 2 && nb16 < 2) continue;
+    if (a.nph > 1 && (a.Cout % (NSUB * 16) || a.Cout % 8)) continue;
+    const int NT = NSUB * 16;
+    const int CoutW = round_up(Nlog, NT);
+    const int nN = CoutW / NT;
+    for (int mi = 0; mi < 3; ++mi) {
+      const int MPW = mpws[mi];
+      GConvArgs c = a;
+      int TX, TY;
+      btile(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
+      c.MPW = MPW;
+      c.NSUB = NSUB;
+      c.CoutW = CoutW;
+      c.TX = TX;
+      c.TY = TY;
+      c.HX = (TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
+      c.HY = (TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
+      c.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
+      const long tiles = (long)cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz * a.B;
+      const int MT = TX * TY * a.TZ;
+      for (int ki = 0; ki < 3; ++ki) {
+        const int CK = cks[ki];
+        if (a.ICs % CK) continue;
+        const long lds = bconv_lds(c, CK, NT);
+        if (lds > lds_cap) continue;
+        const int occ = std::max(1, std::min(2, (int)(160 * 1024 / lds)));
+        const int chunks = a.ICs / CK;
+        const int TPS = 32 / CK;
+        const int S = (T + TPS - 1) / TPS;
+        const double helem = (double)c.HX * c.HY * c.HZ * (CK / 8) / 256.0;
+        const double welem = chunks > 1 ? (double)S * 4 * NT / 256.0 : 0.0;
+        const double t_mfma = (double)S * MPW * NSUB * 16.0;
+        const double t_stage = 1200.0 + 40.0 * (helem + welem);
+        const double hide = occ > 1 ? 0.6 : 1.0;
+        const double t_tile = chunks * (t_mfma + hide * t_stage) + 1500.0 * hide;
+        // blocks: tiles x N blocks (K split added below when this is too few)
+        const double blocks = (double)tiles * nN;
+        const double waves = std::max(1.0, blocks / (256.0 * occ));
+        const double util = (double)MT / (MPW * 64.0) * std::min(1.0, (double)Nlog / CoutW);
+        const double cost = waves * t_tile * occ / std::max(0.25, util) *
+                            (blocks < 256.0 * occ ? 256.0 * occ / blocks * 0.5 + 0.5 : 1.0);
+        if (cost < best) {
+          best = cost;
+          bestA = c;
+          bestA.CK = CK;
+          bestA.lds_bytes = (int)lds;
+          found = true;
+        }
       }
     }
   }
+  if (!found) return fail(4, "bconv: no tile fits in LDS");
+  a = bestA;
+  const int NT = a.NSUB * 16;
+  const int nN = a.CoutW / NT;
   a.ntx = cdiv(a.OX, a.TX);
   a.nty = cdiv(a.OY, a.TY);
   a.ntz = ntz;
-  if (!a.CK) return fail(4, "bconv: no tile fits in LDS");
   const long tiles = (long)a.ntx * a.nty * a.ntz * a.B;
   const int nchunks = a.ICs / a.CK;
   int ks = 1;
-  const int ks_target = env_int_b("HCU_BCONV_KS_TARGET", 512);
+  const int ks_target = env_int_b("HCU_BCONV_KS_TARGET", 256);
   if (a.nph == 1 && 256 % (a.OCs / 8) == 0)
     while (ks < nchunks && tiles * nN * ks < ks_target) ks *= 2;
   ks = std::min(ks, nchunks);
@@ -647,7 +712,7 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   const long nel = (long)a.HX * a.HY * a.HZ * (a.CK / 8);
   const long per_thread = (nel + 255) / 256;
   a.NPF = per_thread <= 4 ? 4 : per_thread <= 8 ? 8 : per_thread <= 12 ? 12 : per_thread <= 16 ? 16 : 0;
-  const int occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
+  const int occ = std::max(1, std::min(2, (int)(160 * 1024 / a.lds_bytes)));
   const long slots = (long)256 * occ;
   const long per_tile = (long)nN * a.ksplit;
   a.gridx = (int)std::min(tiles, std::max(1L, slots / per_tile));

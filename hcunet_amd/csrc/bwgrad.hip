@@ -141,7 +141,10 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
   const uint16_t *Ab = reinterpret_cast<const uint16_t *>(a.A);
   const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
 
-  for (int tt = blockIdx.x; tt < total; tt += gridDim.x) {
+  // contiguous tile range per block (consecutive tiles share halo rows in L2)
+  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_end = min(total, (int)blockIdx.x * tpb_ + tpb_);
+  for (int tt = blockIdx.x * tpb_; tt < t_end; ++tt) {
     const int b = tt / ntiles;
     int tile = tt - b * ntiles;
     const int tzi = tile % a.ntz;

@@ -437,9 +437,12 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
         pf[u] = val;
       }
     };
-    int tile = blockIdx.x;
-    if (tile < total) load_tile(tile);
-    for (; tile < total; tile += gridDim.x) {
+    // contiguous tile range per block (consecutive tiles share halo rows in L2)
+    const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int t_end = min(total, (int)blockIdx.x * tpb_ + tpb_);
+    int tile = blockIdx.x * tpb_;
+    if (tile < t_end) load_tile(tile);
+    for (; tile < t_end; ++tile) {
       int b, ox0, oy0, oz0;
       tile_origin(tile, b, ox0, oy0, oz0);
       __syncthreads();
@@ -447,7 +450,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
       for (int u = 0; u < NPF; ++u)
         if (hpk[u] >= 0) *reinterpret_cast<float4 *>(alds + dst0 + u * VS * CKP) = pf[u];
       __syncthreads();
-      if (tile + (int)gridDim.x < total) load_tile(tile + gridDim.x);
+      if (tile + 1 < t_end) load_tile(tile + 1);
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
 #pragma unroll
@@ -456,7 +459,9 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
       finish_tile(b, ox0, oy0, oz0);
     }
   } else {
-    for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int t_end = min(total, (int)blockIdx.x * tpb_ + tpb_);
+    for (int tile = blockIdx.x * tpb_; tile < t_end; ++tile) {
       int b, ox0, oy0, oz0;
       tile_origin(tile, b, ox0, oy0, oz0);
       const int gx0 = ox0 * a.sx - a.px, gy0 = oy0 * a.sy - a.py, gz0 = oz0 * a.sz - a.pz;

@@ -178,10 +178,13 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       okbits |= (ok ? 1u : 0u) << u;
     }
   };
-  if (blockIdx.x < total) fetch(blockIdx.x);
+  // contiguous tile range per block (consecutive tiles share halo rows in L2)
+  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
+  if (t_beg < t_end) fetch(t_beg);
   if (a.dbg & 32) return;
 
-  for (int tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  for (int tile = t_beg; tile < t_end; ++tile) {
     int b, r, tzi, tyi, txi;
     a.fNT.divmod(tile, b, r);
     a.fNTZ.divmod(r, r, tzi);
@@ -205,7 +208,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       if (!(a.dbg & 16)) *reinterpret_cast<floatx4 *>(alds + (size_t)slot * 4) = ok ? v : z;
     }
     __syncthreads();
-    if (tile + (int)gridDim.x < total) fetch(tile + gridDim.x);
+    if (tile + 1 < t_end) fetch(tile + 1);
     // ---- MFMA over the K-steps, next step's fragments loaded ahead
     floatx4 acc[G];
 #pragma unroll

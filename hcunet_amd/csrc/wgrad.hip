@@ -312,7 +312,9 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
   const int HAV = a.HAX * a.HAY * a.HAZ;        // real halo extent
   const int PTr = a.TX * a.TY * a.TZ;           // real tile extent
 
-  for (int tt = blockIdx.x; tt < total; tt += gridDim.x) {
+  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_end = min(total, (int)blockIdx.x * tpb_ + tpb_);
+  for (int tt = blockIdx.x * tpb_; tt < t_end; ++tt) {
     const int b = tt / ntiles;
     int tile = tt - b * ntiles;
     const int tzi = tile % a.ntz;

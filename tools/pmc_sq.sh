@@ -1,8 +1,9 @@
 #!/usr/bin/env bash
 # SQ counter passes over a short bench run (one rocprofv3 run per pass, counters only).
-#   bash tools/pmc_sq.sh TAG
+#   bash tools/pmc_sq.sh TAG [CONFIG]
 set -o pipefail
 TAG=${1:-sq}
+CFG=${2:-2}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out
 mkdir -p $O
@@ -18,7 +19,7 @@ for P in "$P1" "$P2"; do
   for c in $P; do grep -qx "$c" $O/${TAG}_sq_names.txt || { echo "missing counter $c"; ok=0; }; done
   [ $ok = 1 ] || continue
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/${TAG}_p$i \
-    -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
     > $O/${TAG}_p$i.log 2>&1 || { tail -20 $O/${TAG}_p$i.log; exit 1; }
 done
 python3 tools/pmc_summary.py $O/${TAG}_p1 $O/${TAG}_p2 --top 30 > $O/${TAG}_summary.txt 2>&1
