@@ -40,6 +40,21 @@
 
 namespace hcu {
 
+#ifdef HCU_BCONV_PHASES
+// Per-phase cycle totals of wave 0 of every block (tools/bconv_bench only):
+// [0] halo -> LDS (incl. the wait for the prefetch), [1] barrier + weights,
+// [2] next-halo issue, [3] MFMA loop, [4] epilogue, [5] tiles.
+__device__ unsigned long long g_bconv_phase[8];
+#define PH_MARK(k)                                      \
+  do {                                                  \
+    const long long t__ = (long long)__builtin_readcyclecounter(); \
+    ph_acc[k] += t__ - ph_t;                            \
+    ph_t = t__;                                         \
+  } while (0)
+#else
+#define PH_MARK(k) do {} while (0)
+#endif
+
 namespace {
 // Halo row stride (bf16 elements).  ds_read_b128 serves a wave in 4 lane
 // groups of 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...); with CK = 32 the
@@ -49,16 +64,24 @@ namespace {
 constexpr int ckp_of(int CK) { return CK == 8 ? 8 : (CK == 16 ? 24 : CK + 16); }
 }
 
-template <int CK, int NSUB, int MPW, int NPF>
+// BNB: the input-gradient epilogue fused with the BatchNorm backward (a.bn_y
+// set); a template parameter so that its loads never share registers (and
+// therefore waits) with the other epilogues.
+template <int CK, int NSUB, int MPW, int NPF, bool BNB>
 __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  // launch constants for the tile loop, read through kuni (common.h): they are
+  // live only in the phase that uses them, not for the whole kernel
+  __shared__ __attribute__((aligned(16))) char sa_raw[sizeof(GConvArgs)];
+  GConvArgs &sa = *reinterpret_cast<GConvArgs *>(sa_raw);
+#define KA(f) kuni(sa.f)
   constexpr int NT = NSUB * 16;
   constexpr int C8 = CK / 8;           // 16-byte channel groups per chunk
   constexpr int TPS = 4 / C8;          // taps per K-step
   constexpr int CKP = ckp_of(CK);      // halo row stride (bf16 elements)
-  constexpr int NTP = NT + 4;          // epilogue tile row stride (floats)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
+  if (tid == 0) sa = a;
   const int T = a.KX * a.KY * a.KZ;
   const int S = (T + TPS - 1) / TPS;
   const int HZ = a.HZ, HYZ = a.HY * a.HZ;
@@ -68,17 +91,17 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   int *toffs = reinterpret_cast<int *>(wlds + S * 4 * NT * 8);    // [S][4]
   int *rowpk = toffs + S * 4;                                     // [MPW*64]
   int *rowoff = rowpk + MPW * 64;                                 // [MPW*64]
-  // per-block coefficients live in LDS, not registers (they are only needed in
-  // short phases): epilogue [6][NT] = bias, bn scale/shift/mean/invstd, stats
-  // pivot per stored column; input activation [2][ICs] = scale, shift
+  // per-block coefficients (LDS, read in short phases): [5][NT] = bias, bn
+  // scale/shift/mean/invstd per stored column; [4][NT] statistics pivots of
+  // each wave; input activation [2][ICs] = scale, shift
   float *coefL = reinterpret_cast<float *>(rowoff + MPW * 64);
-  float *actL = coefL + 6 * NT;
+  float *pivL = coefL + 5 * NT;
+  float *actL = pivL + 4 * NT;
 
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
   const int n0 = blockIdx.y * NT;
   const int MT = a.TX * a.TY * a.TZ;
-  const int nmsub = (MT + 15) >> 4;
   const int nchunks = a.ICs / CK;
   const int cb = blockIdx.z * a.cps, ce = min(nchunks, cb + a.cps);
   const int nck = ce - cb;
@@ -118,45 +141,41 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
     toffs[e] = off * CKP + ((e & 3) % C8) * 8;
   }
-
-  {
-    int ph0 = 0, c00 = n0;
-    if (a.nph > 1) {
-      ph0 = n0 / a.Cout;
-      c00 = n0 - ph0 * a.Cout;
-    }
-    for (int j = tid; j < NT; j += 256) {
-      const int c = c00 + j;
-      coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
-      const bool bn = a.bn_y && !split && c < a.OCs;
-      coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;
-      coefL[2 * NT + j] = bn ? a.bn_shift[c] : 0.f;
-      coefL[3 * NT + j] = bn ? a.bn_mean[c] : 0.f;
-      coefL[4 * NT + j] = bn ? a.bn_invstd[c] : 0.f;
-      coefL[5 * NT + j] = 0.f;
-    }
-    if (a.in_scale)
-      for (int c = tid; c < a.ICs; c += 256) {
-        actL[c] = a.in_scale[c];
-        actL[a.ICs + c] = a.in_shift[c];
-      }
+  // first stored channel of the block (ConvTranspose3d phases: all NT columns
+  // of a block belong to one phase, the planner requires Cout % NT == 0)
+  const int co0 = a.nph > 1 ? n0 - (n0 / a.Cout) * a.Cout : n0;
+  for (int j = tid; j < NT; j += 256) {
+    const int c = co0 + j;
+    coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
+    const bool bn = a.bn_y && !split && c < a.OCs;
+    coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;
+    coefL[2 * NT + j] = bn ? a.bn_shift[c] : 0.f;
+    coefL[3 * NT + j] = bn ? a.bn_mean[c] : 0.f;
+    coefL[4 * NT + j] = bn ? a.bn_invstd[c] : 0.f;
   }
+  if (a.in_scale)
+    for (int c = tid; c < a.ICs; c += 256) {
+      actL[c] = a.in_scale[c];
+      actL[a.ICs + c] = a.in_shift[c];
+    }
+
   auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
     int r, tzi, tyi, txi;
-    a.fNT.divmod(tile, b, r);
-    a.fNTZ.divmod(r, r, tzi);
-    a.fNTY.divmod(r, txi, tyi);
-    ox0 = txi * a.TX;
-    oy0 = tyi * a.TY;
-    oz0 = tzi * a.TZ;
+    sa.fNT.uni().divmod(tile, b, r);
+    sa.fNTZ.uni().divmod(r, r, tzi);
+    sa.fNTY.uni().divmod(r, txi, tyi);
+    ox0 = txi * KA(TX);
+    oy0 = tyi * KA(TY);
+    oz0 = tzi * KA(TZ);
   };
   auto stage_w = [&](int chunk) {
     const int n16 = S * 4 * NT;
-    const uint4 *src = reinterpret_cast<const uint4 *>(a.w);
+    const uint4 *src = reinterpret_cast<const uint4 *>(KA(w));
+    const int CoutW = KA(CoutW);
     for (int idx = tid; idx < n16; idx += 256) {
       const int n = idx % NT, sg = idx / NT;
       reinterpret_cast<uint4 *>(wlds)[sg * NT + n] =
-          src[((size_t)chunk * S * 4 + sg) * a.CoutW + n0 + n];
+          src[((size_t)chunk * S * 4 + sg) * CoutW + blockIdx.y * NT + n];
     }
   };
 
@@ -177,21 +196,20 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       hpk[u] = (hx << 20) | (hy << 10) | hz;
     }
   }
-  const uint32_t bX = (uint32_t)a.IY * a.IZ * a.ICs * 2, bY = (uint32_t)a.IZ * a.ICs * 2,
-                 bZ = (uint32_t)a.ICs * 2;
-  const int sample_bytes = a.IX * a.IY * a.IZ * a.ICs * 2;
   const bool act = a.in_scale != nullptr;
   uint4 pf[NPFR];
   uint32_t okbits = 0;
+  // halo of (tile, chunk) -> pf (branch-free: the validity of each element is
+  // a mask, invalid elements read offset 0x7ffffff0, outside the buffer -> 0)
   auto fetch = [&](int tile, int chunk) {
     int b, x0, y0, z0;
     tile_origin(tile, b, x0, y0, z0);
-    const int gx0 = x0 * a.sx - a.px, gy0 = y0 * a.sy - a.py, gz0 = z0 * a.sz - a.pz;
-    const bool inb = gx0 >= 0 && gy0 >= 0 && gz0 >= 0 && gx0 + a.HX <= a.IX &&
-                     gy0 + a.HY <= a.IY && gz0 + a.HZ <= a.IZ;
-    const uint16_t *bp = reinterpret_cast<const uint16_t *>(a.in) + (size_t)b * a.IX * a.IY * a.IZ * a.ICs;
+    const int IX = KA(IX), IY = KA(IY), IZ = KA(IZ), ICs = KA(ICs);
+    const uint32_t bZ = (uint32_t)ICs * 2, bY = (uint32_t)IZ * bZ, bX = (uint32_t)IY * bY;
+    const int gx0 = x0 * KA(sx) - KA(px), gy0 = y0 * KA(sy) - KA(py), gz0 = z0 * KA(sz) - KA(pz);
+    const uint16_t *bp = reinterpret_cast<const uint16_t *>(KA(in)) + (size_t)b * IX * bX / 2;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, sample_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, IX * (int)bX, 0x00020000);
     const int base_off = gx0 * (int)bX + gy0 * (int)bY + gz0 * (int)bZ + (chunk * CK + c8 * 8) * 2;
     okbits = 0;
 #pragma unroll
@@ -199,41 +217,42 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       const int hp = hpk[u];
       const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
       const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
-      const bool ok = hp >= 0 && (inb || ((unsigned)gx < (unsigned)a.IX &&
-                                          (unsigned)gy < (unsigned)a.IY &&
-                                          (unsigned)gz < (unsigned)a.IZ));
+      const bool ok = (hp >= 0) & ((unsigned)gx < (unsigned)IX) & ((unsigned)gy < (unsigned)IY) &
+                      ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      okbits |= (ok ? 1u : 0u) << u;
+      okbits |= (uint32_t)ok << u;
     }
   };
-  // BatchNorm+ReLU of 8 channels (fp32), 0 outside the input
-  // BatchNorm+ReLU of 8 channels (fp32; coefficients from LDS), 0 outside the input
+  // BatchNorm+ReLU of 8 channels: fp32 fused multiply-add (v_pk_fma_f32),
+  // rounded to bf16, ReLU on the packed bf16 (v_pk_max_i16: a bf16 is negative
+  // exactly when its int16 image is); 0 outside the input
   auto activate = [&](uint4 v, bool ok, int chunk) -> uint4 {
     if (!ok) return make_uint4(0u, 0u, 0u, 0u);
     if (!act) return v;
     const int c = chunk * CK + c8 * 8;
-    const float4 s0 = *reinterpret_cast<const float4 *>(actL + c);
-    const float4 s1 = *reinterpret_cast<const float4 *>(actL + c + 4);
-    const float4 h0 = *reinterpret_cast<const float4 *>(actL + a.ICs + c);
-    const float4 h1 = *reinterpret_cast<const float4 *>(actL + a.ICs + c + 4);
-    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-    const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-    float f[8];
-    unpack8(v, f);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) f[k] = fmaxf(fmaf(f[k], sc[k], sh[k]), 0.f);
-    return pack8(f);
+    const int ICs = KA(ICs);
+    const floatx4 s0 = *reinterpret_cast<const floatx4 *>(actL + c);
+    const floatx4 s1 = *reinterpret_cast<const floatx4 *>(actL + c + 4);
+    const floatx4 h0 = *reinterpret_cast<const floatx4 *>(actL + ICs + c);
+    const floatx4 h1 = *reinterpret_cast<const floatx4 *>(actL + ICs + c + 4);
+    uint4 o;
+    o.x = bn_relu_bf2(v.x, s0.xy, h0.xy);
+    o.y = bn_relu_bf2(v.y, s0.zw, h0.zw);
+    o.z = bn_relu_bf2(v.z, s1.xy, h1.xy);
+    o.w = bn_relu_bf2(v.w, s1.zw, h1.zw);
+    return o;
   };
   // direct (non-prefetched) staging of one (tile, chunk) halo
   auto stage_direct = [&](int tile, int chunk) {
     int b, x0, y0, z0;
     tile_origin(tile, b, x0, y0, z0);
     const int gx0 = x0 * a.sx - a.px, gy0 = y0 * a.sy - a.py, gz0 = z0 * a.sz - a.pz;
+    const uint32_t bZ = (uint32_t)a.ICs * 2, bY = (uint32_t)a.IZ * bZ, bX = (uint32_t)a.IY * bY;
     const uint16_t *bp = reinterpret_cast<const uint16_t *>(a.in) + (size_t)b * a.IX * a.IY * a.IZ * a.ICs;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, sample_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, a.IX * (int)bX, 0x00020000);
     for (int base = tid / C8; base < HV; base += 4 * VS) {
       uint4 val[4];
       bool okv[4];
@@ -260,6 +279,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
   };
 
+  // Accumulators hold the transposed tile: the MFMA is issued with the weights
+  // as A and the activations as B, so acc[j][n][r] = out[voxel (wave+4j)*16 +
+  // r16][column n*16 + 4g + r] and every lane owns 4 consecutive channels of
+  // one voxel -> 8-byte stores straight from the accumulators, no LDS round trip.
   floatx4 acc[MPW][NSUB];
   auto load_frag = [&](int s, int toff, shortx8 (&bfr)[NSUB], shortx8 (&afr)[MPW]) {
     const int ss = min(s, S - 1);
@@ -275,7 +298,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     for (int j = 0; j < MPW; ++j)
 #pragma unroll
       for (int n = 0; n < NSUB; ++n)
-        acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[j], bfr[n], acc[j][n], 0, 0, 0);
+        acc[j][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], afr[j], acc[j][n], 0, 0, 0);
   };
   auto compute = [&]() {
     shortx8 b0[NSUB], a0[MPW], b1[NSUB], a1[MPW];
@@ -294,142 +317,174 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
   };
 
-  // ---- epilogue (through LDS, 8 channels = 16 bytes per store)
-  const int nc8 = a.nc4;                 // 8-channel groups of the block's stored columns
-  const int ec8 = tid % nc8;
-  int ph = 0, co0 = n0;
-  if (a.nph > 1) {
-    ph = n0 / a.Cout;
-    co0 = n0 - ph * a.Cout;
-  }
-  const int qz = ph % a.phz, qy = (ph / a.phz) % a.phy, qx = ph / (a.phz * a.phy);
-  const int cst = co0 + ec8 * 8;         // first stored channel of this thread
-  const bool cok = cst < a.OCs;
-  const bool fwdstat = a.stats && !a.bn_y && !split;
-  float st1[8], st2[8], cnt = 0.f;
+  // ---- epilogue: straight from the accumulators.  Every lane issues exactly
+  // MPW * NSUB stores (and, for the fused BatchNorm backward, as many loads)
+  // per tile, invalid ones at an offset outside the buffer (dropped), so the
+  // wait for the next halo can count its loads exactly.
+  const bool fwdstat = a.stats && !BNB && !split;
+  float st1[NSUB][4], st2[NSUB][4], cnt = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) st1[k] = st2[k] = 0.f;
-  bool have_piv = false;
-  // 8 consecutive LDS floats of coefficient array q for this thread's channels
-  auto coef8 = [&](int q, float (&o)[8]) {
-    const float4 c0 = *reinterpret_cast<const float4 *>(coefL + q * NT + ec8 * 8);
-    const float4 c1 = *reinterpret_cast<const float4 *>(coefL + q * NT + ec8 * 8 + 4);
-    o[0] = c0.x; o[1] = c0.y; o[2] = c0.z; o[3] = c0.w;
-    o[4] = c1.x; o[5] = c1.y; o[6] = c1.z; o[7] = c1.w;
-  };
-  float *dstf = split ? a.partial + (size_t)blockIdx.z * a.slice_floats : nullptr;
-  uint16_t *dsth = reinterpret_cast<uint16_t *>(a.out);
-  const uint16_t *ybf = reinterpret_cast<const uint16_t *>(a.bn_y);
-  auto epilogue = [&](int b, int ox0, int oy0, int oz0) {
-    __syncthreads();   // every wave is done reading the halo image
+  for (int n = 0; n < NSUB; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st1[n][r] = st2[n][r] = 0.f;
+  auto epilogue = [&](int b, int ox0, int oy0, int oz0, bool first) {
+    int qx = 0, qy = 0, qz = 0;
+    if (KA(nph) > 1) {
+      const int ph = blockIdx.y * NT / KA(Cout), phz = KA(phz), phy = KA(phy);
+      qz = ph % phz;
+      qy = (ph / phz) % phy;
+      qx = ph / (phz * phy);
+    }
+    const int OX = KA(OX), OY = KA(OY), OZ = KA(OZ), OCs = KA(OCs);
+    const bool interior = ox0 + KA(TX) <= OX && oy0 + KA(TY) <= OY && oz0 + KA(TZ) <= OZ;
+    const int sample = KA(SX) * KA(SY) * KA(SZ) * OCs;
+    const int tb = (((ox0 * KA(osx) + KA(ofx) + qx) * KA(SY) + oy0 * KA(osy) + KA(ofy) + qy) * KA(SZ) +
+                    oz0 * KA(osz) + KA(ofz) + qz) * OCs + co0;
+    const size_t sb = (size_t)b * sample;
+    const int es = split ? 4 : 2;
+    void *obase = split ? (void *)(KA(partial) + (size_t)blockIdx.z * KA(slice_floats) + sb)
+                        : (void *)(reinterpret_cast<uint16_t *>(KA(out)) + sb);
+    const __amdgpu_buffer_rsrc_t ors =
+        __builtin_amdgcn_make_buffer_rsrc(obase, 0, sample * es, 0x00020000);
+    const uint16_t *ybf = reinterpret_cast<const uint16_t *>(KA(bn_y));
+    constexpr bool bnb = BNB;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        bnb ? (void *)(ybf + sb) : obase, 0, bnb ? sample * 2 : 0, 0x00020000);
 #pragma unroll
     for (int j = 0; j < MPW; ++j) {
-      const int m = wave + 4 * j;
-      if (m < nmsub) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int n = 0; n < NSUB; ++n)
-            smem[(m * 16 + g * 4 + r) * NTP + n * 16 + r16] = acc[j][n][r];
-      }
-    }
-    __syncthreads();
-    float bias8[8], piv[8];
-    coef8(0, bias8);
-    if (fwdstat && !have_piv) {   // pivot: the block's first output voxel (row 0)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) piv[k] = smem[ec8 * 8 + k] + bias8[k];
-      if (tid < nc8)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) coefL[5 * NT + ec8 * 8 + k] = piv[k];
-      have_piv = true;
-    } else {
-      coef8(5, piv);
-    }
-    const size_t tbase =
-        ((((size_t)b * a.SX + ox0 * a.osx + a.ofx + qx) * a.SY + oy0 * a.osy + a.ofy + qy) * a.SZ +
-         oz0 * a.osz + a.ofz + qz) * a.OCs + cst;
-    const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
-    const int vstep = 256 / nc8;
-    for (int i = tid / nc8; i < MT; i += vstep) {
-      bool ok = cok;
+      const int i = (wave + 4 * j) * 16 + r16;
+      const int ro = rowoff[i];
+      bool vok = ro >= 0;
       if (!interior) {
         const int pk = rowpk[i];
-        ok = ok && ox0 + (pk >> 20) < a.OX && oy0 + ((pk >> 10) & 1023) < a.OY &&
-             oz0 + (pk & 1023) < a.OZ;
+        vok = vok & (ox0 + (pk >> 20) < OX) & (oy0 + ((pk >> 10) & 1023) < OY) &
+              (oz0 + (pk & 1023) < OZ);
       }
-      if (!ok) continue;
-      const float4 v0 = *reinterpret_cast<const float4 *>(smem + i * NTP + ec8 * 8);
-      const float4 v1 = *reinterpret_cast<const float4 *>(smem + i * NTP + ec8 * 8 + 4);
-      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      const size_t off = tbase + rowoff[i];
-      if (split) {
-        *reinterpret_cast<float4 *>(dstf + off) = v0;
-        *reinterpret_cast<float4 *>(dstf + off + 4) = v1;
-        continue;
-      }
+      const int rof = tb + ro;
+      u32x2 yv[NSUB];
+      if (bnb)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] += bias8[k];
-      if (a.bn_y) {   // fused BatchNorm+ReLU backward: v = dA -> dz; (dz, dz*xhat)
-        float y[8], bsc[8], bsh[8], bmu[8], bis[8];
-        coef8(1, bsc);
-        coef8(2, bsh);
-        coef8(3, bmu);
-        coef8(4, bis);
-        unpack8(*reinterpret_cast<const uint4 *>(ybf + off), y);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          v[k] = fmaf(y[k], bsc[k], bsh[k]) > 0.f ? v[k] : 0.f;
-          st1[k] += v[k];
-          st2[k] = fmaf(v[k], (y[k] - bmu[k]) * bis[k], st2[k]);
+        for (int n = 0; n < NSUB; ++n) {
+          const int col = n * 16 + g * 4;
+          const bool ok = vok & (co0 + col < OCs);
+          yv[n] = __builtin_bit_cast(
+              u32x2, __builtin_amdgcn_raw_buffer_load_b64(yrs, ok ? (rof + col) * 2 : 0x3ffffff0, 0, 0));
         }
-      } else {
+      if (fwdstat && first && j == 0) {
+        // statistics pivot of this wave: its first voxel (+ bias), or the bias
+        // when that voxel lies outside the output
+        const int src = lane & 48;
+        const bool pok = __shfl(vok ? 1 : 0, src) != 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float d = v[k] - piv[k];
-          st1[k] += d;
-          st2[k] = fmaf(d, d, st2[k]);
+        for (int n = 0; n < NSUB; ++n) {
+          const floatx4 bias = *reinterpret_cast<const floatx4 *>(coefL + n * 16 + g * 4);
+          floatx4 p;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) p[r] = bias[r] + (pok ? __shfl(acc[0][n][r], src) : 0.f);
+          if (r16 == 0) *reinterpret_cast<floatx4 *>(pivL + wave * NT + n * 16 + g * 4) = p;
         }
       }
-      cnt += 1.f;
-      *reinterpret_cast<uint4 *>(dsth + off) = pack8(v);
+      if (vok) cnt += 1.f;
+#pragma unroll
+      for (int n = 0; n < NSUB; ++n) {
+        const int col = n * 16 + g * 4;
+        const bool ok = vok & (co0 + col < OCs);
+        const int off = ok ? rof + col : 0x1fffffff;
+        floatx4 v = acc[j][n];
+        if (split) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ors, off * 4, 0, 0);
+          continue;
+        }
+        v += *reinterpret_cast<const floatx4 *>(coefL + col);
+        if (bnb) {   // fused BatchNorm+ReLU backward: v = dA -> dz; (dz, dz*xhat)
+          const u32x2 yw = yv[n];
+          const float y[4] = {bf_lo(yw.x), bf_hi(yw.x), bf_lo(yw.y), bf_hi(yw.y)};
+          const floatx4 bsc = *reinterpret_cast<const floatx4 *>(coefL + NT + col);
+          const floatx4 bsh = *reinterpret_cast<const floatx4 *>(coefL + 2 * NT + col);
+          const floatx4 bmu = *reinterpret_cast<const floatx4 *>(coefL + 3 * NT + col);
+          const floatx4 bis = *reinterpret_cast<const floatx4 *>(coefL + 4 * NT + col);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = (ok && fmaf(y[r], bsc[r], bsh[r]) > 0.f) ? v[r] : 0.f;
+            st1[n][r] += v[r];
+            st2[n][r] = fmaf(v[r], (y[r] - bmu[r]) * bis[r], st2[n][r]);
+          }
+        } else if (fwdstat) {
+          const floatx4 piv = *reinterpret_cast<const floatx4 *>(pivL + wave * NT + col);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = ok ? v[r] - piv[r] : 0.f;
+            st1[n][r] += d;
+            st2[n][r] = fmaf(d, d, st2[n][r]);
+          }
+        }
+        const u32x2 pk2 = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+        __builtin_amdgcn_raw_buffer_store_b64(pk2, ors, off * 2, 0, 0);
+      }
     }
   };
 
-  // ---- main loop over (tile, chunk) items
-  // contiguous tile range per block: consecutive tiles share halo rows, which
-  // then come from this CU's L1/L2 instead of HBM
+  // The epilogue issues MPW*NSUB stores after the next halo's loads.  So that
+  // every path into a halo wait has at least as many younger stores (first
+  // tile, further channel chunks), as many stores to an empty buffer (dropped)
+  // follow every fetch; the compiler's vmcnt for each prefetched element then
+  // does not include the epilogue's stores.
+  auto dummy_epilogue = [&]() {
+    const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, 0, 0x00020000);
+    const u32x2 z = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < MPW * NSUB; ++k) __builtin_amdgcn_raw_buffer_store_b64(z, zr, 32 * k, 0, 0);
+  };
+
+  lds_barrier();   // sa, tables and coefficients are in LDS
+  // ---- main loop over (tile, chunk) items; contiguous tile range per block:
+  // consecutive tiles share halo rows, which then come from this CU's L2
   const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
   const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
+#ifdef HCU_BCONV_PHASES
+  long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
+  long long ph_t = (long long)__builtin_readcyclecounter();
+#endif
+  bool first = true;
   if (NPF > 0) {
     int tile = t_beg;
-    if (tile < t_end) fetch(tile, cb);
     if (nck == 1) stage_w(cb);
+    if (tile < t_end) fetch(tile, cb);
+    dummy_epilogue();
     for (; tile < t_end; ++tile) {
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
 #pragma unroll
         for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
-        for (int u = 0; u < NPFR; ++u)
-          if (hpk[u] >= 0)
-            *reinterpret_cast<uint4 *>(alds + (tid / C8 + u * VS) * CKP + c8 * 8) =
-                activate(pf[u], (okbits >> u) & 1u, chunk);
+        for (int u = 0; u < NPFR; ++u)   // every element is written (the waits stay exact)
+          *reinterpret_cast<uint4 *>(alds + (hpk[u] >= 0 ? (tid / C8 + u * VS) * CKP + c8 * 8 : HV * CKP)) =
+              activate(pf[u], (okbits >> u) & 1u, chunk);
+        PH_MARK(0);
         if (nck > 1) stage_w(chunk);
-        __syncthreads();
+        lds_barrier();
+        PH_MARK(1);
         int nt = tile, nc = chunk + 1;
         if (nc == ce) {
           nc = cb;
           nt = tile + 1;
         }
         if (nt < t_end) fetch(nt, nc);
+        PH_MARK(2);
         compute();
+        PH_MARK(3);
+        dummy_epilogue();   // unconditional: a branch here would be a path without it
       }
       int b, ox0, oy0, oz0;
       tile_origin(tile, b, ox0, oy0, oz0);
-      epilogue(b, ox0, oy0, oz0);
+      epilogue(b, ox0, oy0, oz0, first);
+      first = false;
+      PH_MARK(4);
+#ifdef HCU_BCONV_PHASES
+      ph_acc[5] += 1;
+#endif
     }
   } else {
     for (int tile = t_beg; tile < t_end; ++tile) {
@@ -438,43 +493,58 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
-        __syncthreads();
+        lds_barrier();
         stage_direct(tile, chunk);
+        PH_MARK(0);
         stage_w(chunk);
-        __syncthreads();
+        lds_barrier();
+        PH_MARK(1);
         compute();
+        PH_MARK(3);
       }
       int b, ox0, oy0, oz0;
       tile_origin(tile, b, ox0, oy0, oz0);
-      epilogue(b, ox0, oy0, oz0);
+      epilogue(b, ox0, oy0, oz0, first);
+      first = false;
+      PH_MARK(4);
+#ifdef HCU_BCONV_PHASES
+      ph_acc[5] += 1;
+#endif
     }
   }
+#ifdef HCU_BCONV_PHASES
+  if (tid == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_bconv_phase[k], (unsigned long long)ph_acc[k]);
+#endif
 
-  // ---- statistics rows: fixed-order combine of the threads of a channel group
+  // ---- statistics rows, one per (block, wave): fixed-order butterfly over the
+  // 16 voxel lanes of each channel group, lane r16 == 0 writes
   if (!a.stats || split) return;
-  float *red = smem;   // [256][3]
-  for (int k = 0; k < 8; ++k) {
-    __syncthreads();
-    red[tid * 3 + 0] = st1[k];
-    red[tid * 3 + 1] = st2[k];
-    red[tid * 3 + 2] = cnt;
-    __syncthreads();
-    if (tid < nc8) {
-      float t1 = 0.f, t2 = 0.f, tn = 0.f;
-      for (int q = tid; q < 256; q += nc8) {
-        t1 += red[q * 3 + 0];
-        t2 += red[q * 3 + 1];
-        tn += red[q * 3 + 2];
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) {
+    cnt += __shfl_xor(cnt, m);
+#pragma unroll
+    for (int n = 0; n < NSUB; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st1[n][r] += __shfl_xor(st1[n][r], m);
+        st2[n][r] += __shfl_xor(st2[n][r], m);
       }
-      const int c = n0 + tid * 8 + k;
-      const size_t row = blockIdx.x;
+  }
+  if (r16 != 0) return;
+  const size_t row = (size_t)blockIdx.x * 4 + wave;
+#pragma unroll
+  for (int n = 0; n < NSUB; ++n) {
+    const int col = n * 16 + g * 4;
+    if (co0 + col >= a.OCs) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = n0 + col + r;
       if (fwdstat)
         *reinterpret_cast<float4 *>(a.stats + (row * a.CoutW + c) * 4) =
-            make_float4(t1, t2, coefL[5 * NT + tid * 8 + k], tn);
-      else {
-        a.stats[(row * a.CoutW + c) * 2 + 0] = t1;
-        a.stats[(row * a.CoutW + c) * 2 + 1] = t2;
-      }
+            make_float4(st1[n][r], st2[n][r], cnt > 0.f ? pivL[wave * NT + col + r] : 0.f, cnt);
+      else
+        *reinterpret_cast<float2 *>(a.stats + (row * a.CoutW + c) * 2) = make_float2(st1[n][r], st2[n][r]);
     }
   }
 }
@@ -589,18 +659,17 @@ static void btile(int OX, int OY, int TZ, int maxM, int &TX, int &TY) {
 
 static long bconv_areg(const GConvArgs &a, int CK, int NT) {
   const long HV = (long)a.HX * a.HY * a.HZ;
-  const long halo_f = (HV * ckp_of(CK) + 1) / 2;       // bf16 image, in floats
-  const long ctile = (long)a.MPW * 64 * (NT + 4);      // fp32 epilogue tile
-  return (std::max(halo_f, ctile) + 3) & ~3L;
+  const long halo_f = (HV * ckp_of(CK) + 1) / 2 + 4;   // bf16 image + a dummy 16-byte slot
+  (void)NT;
+  return (halo_f + 3) & ~3L;
 }
 
 static long bconv_lds(const GConvArgs &a, int CK, int NT) {
   const int T = a.KX * a.KY * a.KZ;
   const int TPS = 32 / CK;
   const int S = (T + TPS - 1) / TPS;
-  return std::max(bconv_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128 +
-                      6L * NT + 2L * a.ICs,
-                  256L * 3) * 4;
+  return (bconv_areg(a, CK, NT) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128 + 9L * NT +
+          2L * a.ICs) * 4 + (long)sizeof(GConvArgs);   // + the static copy of the arguments
 }
 
 static int reduce_vpb(const GConvArgs &a) { return 2 * 256 / (a.OCs / 8); }
@@ -611,13 +680,17 @@ int bconv_stat_rows(const GConvArgs &a) {
     const int vpb = reduce_vpb(a);
     return (int)((nvox + vpb - 1) / vpb);
   }
-  return a.gridx;
+  return a.gridx * 4;   // one row per (block, wave)
 }
 
 int plan_bconv(GConvArgs &a, int target_blocks) {
   a.use_bconv = 0;
   if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return fail(2, "bconv: empty output grid");
   if (a.ICs % 8 || a.OCs % 8) return fail(4, "bconv: channel strides must be multiples of 8");
+  // 32-bit buffer offsets within one sample (fp32 K-split partials included)
+  if ((double)a.SX * a.SY * a.SZ * a.OCs * 4 >= 2147483647.0 ||
+      (double)a.IX * a.IY * a.IZ * a.ICs * 2 >= 2147483647.0)
+    return fail(4, "bconv: one sample must stay below 2 GiB");
   if (a.nph < 1) a.nph = 1;
   if (a.phx < 1) a.phx = 1;
   if (a.phy < 1) a.phy = 1;
@@ -637,8 +710,12 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   GConvArgs bestA = a;
   bool found = false;
   const int mpws[3] = {4, 2, 1}, nsubs[3] = {4, 2, 1}, cks[3] = {32, 16, 8};
+  // HCU_BCONV_FORCE="CK,NSUB,MPW[,NPF]" restricts the search (experiments)
+  int fck = 0, fns = 0, fmp = 0, fpf = -1;
+  if (const char *e = getenv("HCU_BCONV_FORCE")) sscanf(e, "%d,%d,%d,%d", &fck, &fns, &fmp, &fpf);
   for (int ni = 0; ni < 3; ++ni) {
     const int NSUB = nsubs[ni];
+    if (fns && NSUB != fns) continue;
     if (NSUB > 1 && nb16 < NSUB && !(NSUB == 2 && nb16 >= 2)) continue;
     if (NSUB == 4 && nb16 < 4) continue;
     if (NSUB == 2 && nb16 < 2) continue;
@@ -648,6 +725,7 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
     const int nN = CoutW / NT;
     for (int mi = 0; mi < 3; ++mi) {
       const int MPW = mpws[mi];
+      if (fmp && MPW != fmp) continue;
       GConvArgs c = a;
       int TX, TY;
       btile(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
@@ -663,7 +741,7 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
       const int MT = TX * TY * a.TZ;
       for (int ki = 0; ki < 3; ++ki) {
         const int CK = cks[ki];
-        if (a.ICs % CK) continue;
+        if (a.ICs % CK || (fck && CK != fck)) continue;
         const long lds = bconv_lds(c, CK, NT);
         if (lds > lds_cap) continue;
         const int occ = std::max(1, std::min(2, (int)(160 * 1024 / lds)));
@@ -712,6 +790,7 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   const long nel = (long)a.HX * a.HY * a.HZ * (a.CK / 8);
   const long per_thread = (nel + 255) / 256;
   a.NPF = per_thread <= 4 ? 4 : per_thread <= 8 ? 8 : per_thread <= 12 ? 12 : per_thread <= 16 ? 16 : 0;
+  if (fpf >= 0 && (fpf == 0 || fpf >= per_thread)) a.NPF = fpf;
   const int occ = std::max(1, std::min(2, (int)(160 * 1024 / a.lds_bytes)));
   const long slots = (long)256 * occ;
   const long per_tile = (long)nN * a.ksplit;
@@ -742,9 +821,14 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
 
 #define BCONV_CASE(CK_, NS_, MP_, PF_)                                                         \
   if (a.CK == CK_ && a.NSUB == NS_ && a.MPW == MP_ && a.NPF == PF_) {                           \
-    HCU_TIMED(s, "bconv_kernel<" #CK_ "," #NS_ "," #MP_ "," #PF_ ">", fl, by,                     \
-              hipLaunchKernelGGL((bconv_kernel<CK_, NS_, MP_, PF_>), grid, dim3(256),           \
-                                 a.lds_bytes, s, a));                                           \
+    if (a.bn_y)                                                                                 \
+      HCU_TIMED(s, "bconv_kernel<" #CK_ "," #NS_ "," #MP_ "," #PF_ ",bnb>", fl, by,               \
+                hipLaunchKernelGGL((bconv_kernel<CK_, NS_, MP_, PF_, true>), grid, dim3(256),   \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                \
+    else                                                                                        \
+      HCU_TIMED(s, "bconv_kernel<" #CK_ "," #NS_ "," #MP_ "," #PF_ ">", fl, by,                   \
+                hipLaunchKernelGGL((bconv_kernel<CK_, NS_, MP_, PF_, false>), grid, dim3(256),  \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                \
     launched = true;                                                                            \
   }
 #define BCONV_PF(CK_, NS_, MP_)                                                          \

@@ -9,6 +9,11 @@
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef short shortx8 __attribute__((ext_vector_type(8)));   // 8 bf16: one MFMA A/B fragment
 typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef short shortx2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 namespace hcu {
 
@@ -20,8 +25,18 @@ __device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
-  return (uint32_t)__builtin_bit_cast(unsigned short, (__bf16)a) |
-         ((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+  const floatx2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));   // v_cvt_pk_bf16_f32
+}
+// relu(x * s + h) of a packed bf16 pair: fp32 fma (v_pk_fma_f32), rounded to
+// bf16, then the ReLU on the rounded pair with v_pk_max_i16 (a bf16 is
+// negative exactly when its int16 image is; -0 becomes +0)
+__device__ __forceinline__ uint32_t bn_relu_bf2(uint32_t w, floatx2 s, floatx2 h) {
+  floatx2 f = {__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+  f = f * s + h;
+  const shortx2 z = {0, 0};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(
+                                          __builtin_bit_cast(shortx2, pack_bf2(f.x, f.y)), z));
 }
 __device__ __forceinline__ uint16_t f2bf(float a) {
   return __builtin_bit_cast(unsigned short, (__bf16)a);
@@ -53,6 +68,8 @@ struct FastDiv {
   __host__ __device__ __forceinline__ uint32_t div(uint32_t n) const {
     return (uint32_t)((((uint64_t)n * m >> 32) + n) >> s);  // v_mul_hi_u32 on device
   }
+  // the same divisor with its fields read through kuni (see below)
+  __device__ __forceinline__ FastDiv uni() const;
   // q = n / d, r = n % d
   __host__ __device__ __forceinline__ void divmod(uint32_t n, int &q, int &r) const {
     const uint32_t qq = div(n);
@@ -60,6 +77,43 @@ struct FastDiv {
     r = (int)(n - qq * d);
   }
 };
+
+// Uniform value re-materialised into SGPRs from an LDS copy of the launch
+// arguments.  Kernels with many launch constants read them this way inside
+// their tile loops: LDS loads are not hoisted across the loop's barriers, so
+// the constants are live only where used instead of occupying (and spilling)
+// scalar registers for the whole kernel.
+template <class T>
+__device__ __forceinline__ T kuni(const T &v) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "kuni: 4- or 8-byte values");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+  } else {
+    int2 p = __builtin_bit_cast(int2, v);
+    p.x = __builtin_amdgcn_readfirstlane(p.x);
+    p.y = __builtin_amdgcn_readfirstlane(p.y);
+    return __builtin_bit_cast(T, p);
+  }
+}
+
+__device__ __forceinline__ FastDiv FastDiv::uni() const {
+  FastDiv f;
+  f.d = kuni(d);
+  f.m = kuni(m);
+  f.s = kuni(s);
+  return f;
+}
+
+// Workgroup barrier that orders LDS only.  __syncthreads() is a fence on all
+// address spaces: it waits for every outstanding global load AND store
+// (vmcnt(0)) before the barrier, which drains the previous tile's output
+// stores and the next tile's prefetch at every barrier of a persistent loop.
+// Kernels whose barriers only publish LDS data use this instead.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // Thread-local error message (hcu_last_error()).
 void set_error(const std::string &msg);

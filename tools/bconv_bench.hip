@@ -1,0 +1,159 @@
+// Stand-alone timing of one bf16 convolution launch (bconv.hip) with per-phase
+// cycle counts of the persistent tile loop.  Experiment tool, not part of the
+// library or the tests.
+//
+//   tools/bconv_bench.sh            (builds tools/bconv_bench against libhcunet.so)
+//   tools/bconv_bench MODE B IX IY IZ ICs Cout KX KY KZ ACT [ITERS]
+//     MODE f = forward (+ BatchNorm statistics rows), d = input gradient
+//     (padding K-1), db = input gradient with the fused BatchNorm backward
+//     epilogue; ACT 1 = BatchNorm+ReLU applied to the input while staging.
+//   HCU_BCONV_FORCE="CK,NSUB,MPW[,NPF]" pins the tiling.
+#define HCU_BCONV_PHASES 1
+#include "../hcunet_amd/csrc/bconv.hip"
+
+#include <chrono>
+#include <cstring>
+#include <random>
+#include <vector>
+
+namespace hcu {
+// the library's error channel (unet.cpp), stand-alone here
+void set_error(const std::string &msg) { fprintf(stderr, "error: %s\n", msg.c_str()); }
+int fail(int code, const std::string &msg) {
+  set_error(msg);
+  return code;
+}
+}  // namespace hcu
+using namespace hcu;
+
+#define CK_HIP(x)                                                              \
+  do {                                                                         \
+    hipError_t e__ = (x);                                                      \
+    if (e__ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e__)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+static uint16_t to_bf(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+}
+
+template <class T>
+static T *dev_fill(size_t n, std::vector<T> &h) {
+  T *d = nullptr;
+  CK_HIP(hipMalloc(&d, std::max<size_t>(n, 1) * sizeof(T)));
+  if (n) CK_HIP(hipMemcpy(d, h.data(), n * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 12) {
+    fprintf(stderr, "usage: %s MODE B IX IY IZ ICs Cout KX KY KZ ACT [ITERS]\n", argv[0]);
+    return 2;
+  }
+  const std::string mode = argv[1];
+  const int B = atoi(argv[2]), IX = atoi(argv[3]), IY = atoi(argv[4]), IZ = atoi(argv[5]);
+  const int ICs = atoi(argv[6]), Cout = atoi(argv[7]);
+  const int K[3] = {atoi(argv[8]), atoi(argv[9]), atoi(argv[10])};
+  const int act = atoi(argv[11]);
+  const int iters = argc > 12 ? atoi(argv[12]) : 20;
+  const bool dgrad = mode[0] == 'd';
+  const bool bnbwd = mode == "db";
+
+  GConvArgs a{};
+  a.B = B;
+  a.IX = IX; a.IY = IY; a.IZ = IZ; a.ICs = ICs;
+  if (dgrad) {
+    a.OX = IX + K[0] - 1; a.OY = IY + K[1] - 1; a.OZ = IZ + K[2] - 1;
+    a.px = K[0] - 1; a.py = K[1] - 1; a.pz = K[2] - 1;
+  } else {
+    a.OX = IX - K[0] + 1; a.OY = IY - K[1] + 1; a.OZ = IZ - K[2] + 1;
+  }
+  a.SX = a.OX; a.SY = a.OY; a.SZ = a.OZ;
+  a.OCs = (Cout + 7) / 8 * 8;
+  a.Cout = Cout;
+  a.osx = a.osy = a.osz = 1;
+  a.KX = K[0]; a.KY = K[1]; a.KZ = K[2];
+  a.sx = a.sy = a.sz = 1;
+  a.dx = a.dy = a.dz = 1;
+  if (int e = plan_bconv(a, 0)) {
+    fprintf(stderr, "plan failed %d\n", e);
+    return 1;
+  }
+  const int T = K[0] * K[1] * K[2];
+  const int TPS = 32 / a.CK;
+  const int S = (T + TPS - 1) / TPS;
+  const size_t n_in = (size_t)B * IX * IY * IZ * ICs;
+  const size_t n_out = (size_t)B * a.SX * a.SY * a.SZ * a.OCs;
+  const size_t n_w = (size_t)(ICs / a.CK) * S * 4 * a.CoutW * 8;
+  std::mt19937 rng(1);
+  std::uniform_real_distribution<float> U(-1.f, 1.f);
+  std::vector<uint16_t> hin(n_in), hw(n_w), hy(n_out);
+  for (auto &v : hin) v = to_bf(U(rng));
+  for (auto &v : hw) v = to_bf(0.05f * U(rng));
+  for (auto &v : hy) v = to_bf(U(rng));
+  std::vector<float> hsc(ICs, 1.1f), hsh(ICs, 0.05f), hb(Cout, 0.01f), hco(a.OCs, 0.5f);
+  std::vector<uint16_t> none;
+  a.in = reinterpret_cast<const float *>(dev_fill(n_in, hin));
+  a.w = reinterpret_cast<const float *>(dev_fill(n_w, hw));
+  uint16_t *dout = nullptr;
+  CK_HIP(hipMalloc(&dout, n_out * 2));
+  a.out = reinterpret_cast<float *>(dout);
+  a.bias = dev_fill((size_t)Cout, hb);
+  if (act) {
+    a.in_scale = dev_fill((size_t)ICs, hsc);
+    a.in_shift = dev_fill((size_t)ICs, hsh);
+  }
+  if (bnbwd) {
+    a.bn_y = reinterpret_cast<const float *>(dev_fill(n_out, hy));
+    a.bn_scale = dev_fill((size_t)a.OCs, hco);
+    a.bn_shift = dev_fill((size_t)a.OCs, hco);
+    a.bn_mean = dev_fill((size_t)a.OCs, hco);
+    a.bn_invstd = dev_fill((size_t)a.OCs, hco);
+  }
+  if (!dgrad || bnbwd) {
+    const size_t rows = (size_t)bconv_stat_rows(a);
+    CK_HIP(hipMalloc(&a.stats, rows * a.CoutW * 4 * sizeof(float)));
+  }
+  if (a.ksplit > 1) CK_HIP(hipMalloc(&a.partial, (size_t)a.ksplit * a.slice_floats * sizeof(float)));
+
+  hipStream_t s;
+  CK_HIP(hipStreamCreate(&s));
+  for (int i = 0; i < 3; ++i)
+    if (launch_bconv(a, s)) return 1;
+  CK_HIP(hipStreamSynchronize(s));
+  unsigned long long z[8] = {0};
+  CK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bconv_phase), z, sizeof(z)));
+  hipEvent_t e0, e1;
+  CK_HIP(hipEventCreate(&e0));
+  CK_HIP(hipEventCreate(&e1));
+  CK_HIP(hipEventRecord(e0, s));
+  for (int i = 0; i < iters; ++i) launch_bconv(a, s);
+  CK_HIP(hipEventRecord(e1, s));
+  CK_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK_HIP(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long ph[8];
+  CK_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_bconv_phase), sizeof(ph)));
+  const double us = ms * 1e3 / iters;
+  const double flops = 2.0 * B * a.OX * a.OY * a.OZ * (double)Cout * T * ICs;
+  const double bytes = 2.0 * (n_in + n_out) + (bnbwd ? 2.0 * n_out : 0.0);
+  printf("%s B%d I%dx%dx%d ICs%d Cout%d K%dx%dx%d act%d | CK%d NSUB%d MPW%d T%dx%dx%d NPF%d ks%d grid%d "
+         "lds%d | %.1f us  %.1f TF/s  %.0f GB/s\n",
+         mode.c_str(), B, IX, IY, IZ, ICs, Cout, K[0], K[1], K[2], act, a.CK, a.NSUB, a.MPW, a.TX,
+         a.TY, a.TZ, a.NPF, a.ksplit, a.gridx, a.lds_bytes, us, flops / us * 1e-6,
+         bytes / us * 1e-3);
+  double tot = 0;
+  for (int k = 0; k < 5; ++k) tot += (double)ph[k];
+  const double tiles = (double)ph[5];
+  if (tiles <= 0) printf("  no phase counts (raw %llu %llu %llu)\n", ph[0], ph[3], ph[5]);
+  else
+    printf("  per tile (wave 0, cycles): halo->lds %.0f  barrier+w %.0f  fetch %.0f  mfma %.0f  "
+           "epilogue %.0f  total %.0f (tiles/launch %.0f)\n",
+           ph[0] / tiles, ph[1] / tiles, ph[2] / tiles, ph[3] / tiles, ph[4] / tiles, tot / tiles,
+           tiles / iters);
+  return 0;
+}
