@@ -118,6 +118,72 @@ def load_traffic(kernel):
         return None
 
 
+# The network of the reference's inference pipeline (hcat/main.py:46-54) and
+# the tiled driver it runs (hcat/segment.py:21-136), SURVEY §8f-1.
+INFER_KW = dict(image_dimensions=3, in_channels=4, out_channels=1, feature_sizes=[16, 32, 64, 128],
+                kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)}, upsample_kernel=(8, 8, 2),
+                max_pool_kernel=(2, 2, 1), upsample_stride=(2, 2, 1), dilation=1, groups=2)
+INFER_VOLUME = (1, 4, 1024, 1024, 40)
+
+
+def infer_main(args):
+    """Tiled inference throughput: hcat.segment.predict_segmentation_mask over a
+    synthetic fp16 [1, 4, 1024, 1024, 40] volume (to_tensor output dtype) with the
+    main.py network in eval mode, random init; tile size from the device memory
+    (288 GB -> [350, 350, 15] + PAD (128, 128, 10)).  One step = the whole volume."""
+    from hcunet_amd import segment as seg
+    device = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    model = Unet_Constructor(**INFER_KW).to(device).eval()
+    g = torch.Generator().manual_seed(7)
+    vol = ((torch.rand(INFER_VOLUME, generator=g) - 0.5) * 2).half()
+    vol_dev = vol.to(device)
+    ev = seg.eval_image_size(torch.cuda.get_device_properties(device).total_memory)
+    n_tiles = 1
+    for d in range(3):
+        n = INFER_VOLUME[2 + d]
+        e = min(ev[d], n) if d == 2 else ev[d]
+        p = min(seg.PAD_SIZE[d], n)
+        n_tiles *= len(seg.calculate_indexes(seg.PAD_SIZE[d], e, n, n + 2 * p))
+    for _ in range(args.warmup):
+        seg.predict_segmentation_mask(model, vol_dev, device, use_probability_map=True)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mask = seg.predict_segmentation_mask(model, vol_dev, device, use_probability_map=True)
+    torch.cuda.synchronize(device)
+    el = (time.perf_counter() - t0) / args.steps
+    vox = INFER_VOLUME[2] * INFER_VOLUME[3] * INFER_VOLUME[4]
+    cpu = None
+    if not args.no_cpu_baseline:
+        # one tile of the oracle restatement (CPU, B=1, eval) on the host cores
+        from oracle import unet_oracle as uo
+        threads = max(1, min(16, os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        spec = uo.normalize_spec(**INFER_KW)
+        net = uo.OracleUnet(spec, {k: v.detach().cpu() for k, v in model.state_dict().items()})
+        tile = vol[:, :, :ev[0] + 2 * seg.PAD_SIZE[0], :ev[1] + 2 * seg.PAD_SIZE[1],
+                   :ev[2] + 2 * seg.PAD_SIZE[2] - 1].float()
+        with torch.no_grad():
+            net.forward(tile, training=False)
+            t1 = time.perf_counter()
+            net.forward(tile, training=False)
+            tt = time.perf_counter() - t1
+        cpu = {"value": 1.0 / tt, "unit": "tiles/s", "cores": threads, "kind": "port",
+               "sample": "1 eval forward of one %s tile (oracle restatement, torch CPU fp32, "
+                         "%d threads): %.2f s/tile" % ('x'.join(map(str, tile.shape[2:])), threads, tt)}
+    line = {"metric": "tiled inference voxels/sec (predict_segmentation_mask, hcat/main.py network)",
+            "value": vox / el, "unit": "voxels/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": "tiled eval inference of a %s fp16 volume, tiles %s + pad %s, "
+                                   "%d tiles per volume, main.py network [16..128] groups=2 up (8,8,2)"
+                                   % ('x'.join(map(str, INFER_VOLUME)), ev, list(seg.PAD_SIZE), n_tiles),
+                       "tiles_per_s": n_tiles / el, "mask_mean": float(mask.mean())},
+            "cpu_baseline": cpu}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -126,7 +192,11 @@ def main():
     ap.add_argument('--config', default='2', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--infer', action='store_true',
+                    help='tiled inference driver throughput (SURVEY 8f-1) instead of training')
     args = ap.parse_args()
+    if args.infer:
+        return infer_main(args)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

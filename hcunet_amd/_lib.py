@@ -19,6 +19,8 @@ HCU_ERR_UNSUPPORTED = 4
 HCU_ERR_WORKSPACE = 5
 
 HCU_F32, HCU_F16, HCU_U8, HCU_BF16 = 0, 1, 2, 3
+HCU_PLAN_FORWARD_ONLY = 1
+HCU_TILE_BATCH_MAX = 64
 MAX_LEVELS = 12
 
 c_int3 = ctypes.c_int * 3
@@ -82,6 +84,8 @@ SYMBOLS = [
     ("hcu_last_error", ctypes.c_char_p, []),
     ("hcu_version", _I, []),
     ("hcu_unet_plan_create", _I, [ctypes.POINTER(UnetSpec), _I, _I, _I, _I, ctypes.POINTER(_VP)]),
+    ("hcu_unet_plan_create_ex", _I, [ctypes.POINTER(UnetSpec), _I, _I, _I, _I, _I,
+                                     ctypes.POINTER(_VP)]),
     ("hcu_unet_plan_destroy", None, [_VP]),
     ("hcu_unet_plan_query", _I, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I64),
                                  ctypes.POINTER(_I), ctypes.POINTER(_SZ), ctypes.POINTER(_SZ)]),
@@ -99,6 +103,11 @@ SYMBOLS = [
     ("hcu_conv_dgrad_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("hcu_conv_wgrad_cl", _I, [ctypes.POINTER(ConvDesc), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("hcu_maxpool_fwd_cl", _I, [_I, _I, _I, _I, _I, ctypes.POINTER(_I), _VP, _VP, _VP]),
+    ("hcu_tile_gather", _I, [_VP, _I, _I, _I, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), _I,
+                             ctypes.POINTER(_I), _I, _VP, _VP]),
+    ("hcu_tile_scatter", _I, [_VP, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I), _VP,
+                              _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I), _I,
+                              _F, _VP]),
     ("hcu_timing_enable", _I, [_I]),
     ("hcu_timing_disable", _I, []),
     ("hcu_timing_detail", _I, [_I]),

@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
     tile /= a.ntz;
     const int tyi = tile % a.nty, txi = tile / a.nty;
     const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
-    __syncthreads();
+    lds_barrier();
     {  // A halo (channels-last, activation applied, 0 outside the input)
       const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
       const size_t bbase = (size_t)b * a.AX * a.AY * a.AZ;
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
     }
     // ConvTranspose3d: input voxels past the input grid must contribute 0; their
     // A rows are 0 (staged as outside), so nothing else is needed.
-    __syncthreads();
+    lds_barrier();
     for (int p0 = 0; p0 < PT; p0 += 32) {
       const int pr = p0 + 8 * g + q4;
       const int ra0 = hvA[pr], ra1 = hvA[pr + 4];

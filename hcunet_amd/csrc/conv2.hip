@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NSUB; ++n) pivl[n * 16 + r16] = acc[0][n][0] + bias_v[n];
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int n = 0; n < NSUB; ++n) pv[n] = pivl[n * 16 + r16];
       have_piv = true;
@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     bis = *reinterpret_cast<const float4 *>(a.bn_invstd + cc);
   }
   auto epilogue_lds = [&](int b, int ox0, int oy0, int oz0) {
-    __syncthreads();  // every wave is done reading the halo image
+    lds_barrier();  // every wave is done reading the halo image
 #pragma unroll
     for (int j = 0; j < MPW; ++j) {
       const int m = wave + 4 * j;
@@ -325,7 +325,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
             smem[(m * 16 + g * 4 + r) * NTP + n * 16 + r16] = acc[j][n][r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     float *tp = dst + ((((size_t)b * a.SX + ox0 * a.osx + a.ofx) * a.SY + oy0 * a.osy + a.ofy) *
                            a.SZ + oz0 * a.osz + a.ofz) * a.OCs + n0 + ec4 * 4;
     const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
@@ -445,11 +445,11 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     for (; tile < t_end; ++tile) {
       int b, ox0, oy0, oz0;
       tile_origin(tile, b, ox0, oy0, oz0);
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int u = 0; u < NPF; ++u)
         if (hpk[u] >= 0) *reinterpret_cast<float4 *>(alds + dst0 + u * VS * CKP) = pf[u];
-      __syncthreads();
+      lds_barrier();
       if (tile + 1 < t_end) load_tile(tile + 1);
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
@@ -471,7 +471,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
         for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
         const int ci0 = chunk * CK;
-        __syncthreads();
+        lds_barrier();
         for (int base = tid; base < nel; base += 4 * 256) {
           float4 val[4];
 #pragma unroll
@@ -486,7 +486,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
           }
         }
         stage_w(chunk);
-        __syncthreads();
+        lds_barrier();
         compute();
       }
       finish_tile(b, ox0, oy0, oz0);
@@ -496,13 +496,13 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
   if (a.stats && !split && a.epi_lds) {
     // fixed-order combine of the threads that share a channel group (they
     // share the pivot too, so their pivoted sums add)
-    __syncthreads();
+    lds_barrier();
     float *red = smem;  // [256][16]: st1[4], st2[4], cnt, -, -, -, pivot[4]
     red[tid * 16 + 0] = st1.x; red[tid * 16 + 1] = st1.y; red[tid * 16 + 2] = st1.z; red[tid * 16 + 3] = st1.w;
     red[tid * 16 + 4] = st2.x; red[tid * 16 + 5] = st2.y; red[tid * 16 + 6] = st2.z; red[tid * 16 + 7] = st2.w;
     red[tid * 16 + 8] = cnt;
     red[tid * 16 + 12] = piv4.x; red[tid * 16 + 13] = piv4.y; red[tid * 16 + 14] = piv4.z; red[tid * 16 + 15] = piv4.w;
-    __syncthreads();
+    lds_barrier();
     if (tid < nc4 * 4) {
       const int c4 = tid >> 2, comp = tid & 3;
       float t1 = 0.f, t2 = 0.f, tn = 0.f;
@@ -532,7 +532,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
     }
     cnt += __shfl_xor(cnt, 16);
     cnt += __shfl_xor(cnt, 32);
-    __syncthreads();
+    lds_barrier();
     float *red = smem;  // [4][NT][3]
     if (lane < 16) {
 #pragma unroll
@@ -542,7 +542,7 @@ __global__ void __launch_bounds__(256) conv2_kernel(const GConvArgs a) {
         red[(wave * NT + n * 16 + lane) * 3 + 2] = cnt;
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < NT) {
       float t1 = 0.f, t2 = 0.f, tn = 0.f;
 #pragma unroll
@@ -641,11 +641,11 @@ __global__ void __launch_bounds__(256) conv2_reduce_kernel(const GConvArgs a, in
   if (!a.stats) return;
   const float pk[4] = {piv.x, piv.y, piv.z, piv.w};
   for (int comp = 0; comp < 4; ++comp) {
-    __syncthreads();
+    lds_barrier();
     red[tid][0] = st1[comp];
     red[tid][1] = st2[comp];
     red[tid][2] = cnt;
-    __syncthreads();
+    lds_barrier();
     if (tid < C4) {
       float t1 = 0.f, t2 = 0.f, tn = 0.f;
       for (int k = tid; k < 256; k += C4) {

@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     a.fNTZ.divmod(r, r, tzi);
     a.fNTY.divmod(r, txi, tyi);
     const int ox0 = txi * a.TX, oy0 = tyi * a.TY, oz0 = tzi * a.TZ;
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
       const int idx = tid + u * 256;
@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       const int slot = hpk[u] >= 0 ? (idx % C4) * HVP + idx / C4 : C4 * HVP - 1;
       if (!(a.dbg & 16)) *reinterpret_cast<floatx4 *>(alds + (size_t)slot * 4) = ok ? v : z;
     }
-    __syncthreads();
+    lds_barrier();
     if (tile + 1 < t_end) fetch(tile + 1);
     // ---- MFMA over the K-steps, next step's fragments loaded ahead
     floatx4 acc[G];
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     }
     if (fwdstat && !have_piv) {   // block-uniform: the first tile of this block
       if (wave == 0 && ((lane >> 2) & 7) == 0) pivl[col] = acc[0][0] + bias;
-      __syncthreads();
+      lds_barrier();
       piv = pivl[col];
       have_piv = true;
     }
@@ -298,14 +298,14 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   s1 += __shfl_xor(s1, 16);
   s2 += __shfl_xor(s2, 16);
   cnt += __shfl_xor(cnt, 16);
-  __syncthreads();
+  lds_barrier();
   float *red = smem;  // [4 waves][8 channels][3]
   if (((lane >> 2) & 7) == 0) {
     red[(wave * 8 + col) * 3 + 0] = s1;
     red[(wave * 8 + col) * 3 + 1] = s2;
     red[(wave * 8 + col) * 3 + 2] = cnt;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 8) {
     float t1 = 0.f, t2 = 0.f, tn = 0.f;
 #pragma unroll

@@ -250,48 +250,58 @@ int plan_gconv(GConvArgs &a, int target_blocks) {
   if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return fail(2, "gconv: empty output grid");
   if (a.ICs % 4 != 0 || a.OCs % 4 != 0) return fail(1, "gconv: channel strides must be multiples of 4");
   const int T = a.KX * a.KY * a.KZ;
-  a.NSUB = nsub_for(a.Cout);
-  const int NT = a.NSUB * 16;
-  const int NTP = (a.NSUB & 1) ? NT : NT + 16;
-  a.CoutW = round_up(a.Cout, NT);
-  const int ntz = cdiv(a.OZ, 16);
-  a.TZ = cdiv(a.OZ, ntz);
-  const int nchunk = a.CoutW / NT;
-  const int mpws[3] = {4, 2, 1};
-  for (int mi = 0; mi < 3; ++mi) {
-    const int MPW = mpws[mi];
-    int TX, TY;
-    tile_dims(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
-    const int ntx = cdiv(a.OX, TX), nty = cdiv(a.OY, TY);
-    const long blocks = (long)ntx * nty * ntz * nchunk * a.B;
-    if (blocks >= target_blocks || MPW == 1) {
-      a.MPW = MPW;
-      a.TX = TX;
-      a.TY = TY;
-      a.ntx = ntx;
-      a.nty = nty;
-      a.ntz = ntz;
-      break;
-    }
-  }
-  a.HX = (a.TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
-  a.HY = (a.TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
-  a.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
-  const int HV = a.HX * a.HY * a.HZ;
-  a.P = HV + ((16 - HV % 32) + 32) % 32;
-  const int cks[3] = {16, 8, 4};
+  // widest column block first; narrower ones when the weight tile of a large
+  // kernel (e.g. an 8x8x2 ConvTranspose3d input gradient) does not fit in LDS
+  const int ns0 = nsub_for(a.Cout);
+  const int nss[3] = {ns0, std::min(ns0, 2), 1};
   a.CK = 0;
-  for (int ci = 0; ci < 3; ++ci) {
-    const int CK = cks[ci];
-    if (a.ICs % CK) continue;
-    const long lds = ((long)CK * a.P + (long)T * CK * NTP) * 4;
-    if (lds <= 65536) {
-      a.CK = CK;
-      a.lds_bytes = (int)lds;
-      break;
+  for (int ni = 0; ni < 3 && !a.CK; ++ni) {
+    if (ni > 0 && nss[ni] == nss[ni - 1]) continue;
+    a.NSUB = nss[ni];
+    const int NT = a.NSUB * 16;
+    const int NTP = (a.NSUB & 1) ? NT : NT + 16;
+    a.CoutW = round_up(a.Cout, NT);
+    const int ntz = cdiv(a.OZ, 16);
+    a.TZ = cdiv(a.OZ, ntz);
+    const int nchunk = a.CoutW / NT;
+    const int mpws[3] = {4, 2, 1};
+    for (int mi = 0; mi < 3; ++mi) {
+      const int MPW = mpws[mi];
+      int TX, TY;
+      tile_dims(a.OX, a.OY, a.TZ, 64 * MPW, TX, TY);
+      const int ntx = cdiv(a.OX, TX), nty = cdiv(a.OY, TY);
+      const long blocks = (long)ntx * nty * ntz * nchunk * a.B;
+      if (blocks >= target_blocks || MPW == 1) {
+        a.MPW = MPW;
+        a.TX = TX;
+        a.TY = TY;
+        a.ntx = ntx;
+        a.nty = nty;
+        a.ntz = ntz;
+        break;
+      }
+    }
+    a.HX = (a.TX - 1) * a.sx + (a.KX - 1) * a.dx + 1;
+    a.HY = (a.TY - 1) * a.sy + (a.KY - 1) * a.dy + 1;
+    a.HZ = (a.TZ - 1) * a.sz + (a.KZ - 1) * a.dz + 1;
+    const int HV = a.HX * a.HY * a.HZ;
+    a.P = HV + ((16 - HV % 32) + 32) % 32;
+    const int cks[3] = {16, 8, 4};
+    for (int ci = 0; ci < 3; ++ci) {
+      const int CK = cks[ci];
+      if (a.ICs % CK) continue;
+      const long lds = ((long)CK * a.P + (long)T * CK * NTP) * 4;
+      if (lds <= 160 * 1024 - 4096) {   // gfx950: 160 KB of LDS per workgroup
+        a.CK = CK;
+        a.lds_bytes = (int)lds;
+        break;
+      }
     }
   }
-  if (!a.CK) return fail(4, "gconv: no tile fits in LDS");
+  if (!a.CK)
+    return fail(4, "gconv: no tile fits in LDS (K " + std::to_string(a.KX) + "x" + std::to_string(a.KY) + "x" +
+                       std::to_string(a.KZ) + ", ICs " + std::to_string(a.ICs) + ", Cout " + std::to_string(a.Cout) + ")");
+  const int NT = a.NSUB * 16;
   a.fHZ = FastDiv(a.HZ);
   a.fHY = FastDiv(a.HY);
   a.fTZ = FastDiv(a.TZ);

@@ -321,6 +321,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 struct hcu_unet_plan {
   hcu_unet_spec spec;
   int B, X, Y, Z, L;
+  int flags = 0;       // HCU_PLAN_FORWARD_ONLY: activations in two ping-pong buffers
   int es = 4;          // activation element bytes: 4 (fp32 path) or 2 (bf16 path)
   Dims xin;
   size_t xcl_off = 0;
@@ -479,11 +480,23 @@ int build_plan(hcu_unet_plan &p) {
 
   // Shapes, forward order.
   Region saved;
+  // Activation tensors in forward order.  A forward-only plan keeps none of them
+  // for a backward: every forward op reads only the tensor the previous op
+  // wrote (the skip tensors are shape checks only, hcat/unet.py:309-315), so
+  // they alternate between two buffers of the largest activation.
+  const bool fwd_only = (p.flags & HCU_PLAN_FORWARD_ONLY) != 0;
+  std::vector<std::pair<size_t *, size_t>> acts;
+  auto act_take = [&](size_t floats, size_t &off) {
+    if (fwd_only)
+      acts.emplace_back(&off, floats);
+    else
+      off = saved.take_floats(floats);
+  };
   if (s.compute_dtype != HCU_F32 && s.compute_dtype != HCU_BF16)
     return fail(HCU_ERR_INVALID, "compute_dtype must be HCU_F32 or HCU_BF16");
   p.es = s.compute_dtype == HCU_BF16 ? 2 : 4;
   p.xin = mkdims(p.B, p.X, p.Y, p.Z, s.in_channels, p.es);
-  p.xcl_off = saved.take_floats(p.xin.floats());
+  act_take(p.xin.floats(), p.xcl_off);
   p.max_act = p.xin.floats();
   Dims cur = p.xin;
   for (int i = 0; i < L; ++i) {
@@ -491,7 +504,7 @@ int build_plan(hcu_unet_plan &p) {
     if (int e = setup_conv(p.dc1[i], cur, f, s.g1, cin, cin, s.k1, s.d1, "down conv1")) return e;
     if (int e = setup_conv(p.dc2[i], p.dc1[i].out, f, s.g2, f, f, s.k2, s.d2, "down conv2")) return e;
     for (ConvLayer *c : {&p.dc1[i], &p.dc2[i]}) {
-      c->y_off = saved.take_floats(c->out.floats());
+      act_take(c->out.floats(), c->y_off);
       c->bn.coef_off = saved.take_floats((size_t)6 * c->bn.Cs);
       track_conv(p, *c);
     }
@@ -501,7 +514,7 @@ int build_plan(hcu_unet_plan &p) {
       if (px < 1 || py < 1 || pz < 1)
         return fail(HCU_ERR_SHAPE, "max_pool3d: Output size is too small");
       p.pooled[i] = mkdims(p.B, px, py, pz, f, p.es);
-      p.pool_off[i] = saved.take_floats(p.pooled[i].floats());
+      act_take(p.pooled[i].floats(), p.pool_off[i]);
       p.max_act = std::max(p.max_act, p.pooled[i].floats());
       cur = p.pooled[i];
     }
@@ -518,13 +531,13 @@ int build_plan(hcu_unet_plan &p) {
                       std::to_string(u.out.X) + "x" + std::to_string(u.out.Y) + "x" +
                       std::to_string(u.out.Z) + " exceeds skip " + std::to_string(skip.X) + "x" +
                       std::to_string(skip.Y) + "x" + std::to_string(skip.Z) + ")");
-    u.u_off = saved.take_floats(u.out.floats());
+    act_take(u.out.floats(), u.u_off);
     p.max_act = std::max(p.max_act, u.out.floats());
     // conv1 consumes cat(U, U): fold (cat channels 2*o, effective o)
     if (int e = setup_conv(p.uc1[j], u.out, o, s.g1, o, f, s.k1, s.d1, "up conv1")) return e;
     if (int e = setup_conv(p.uc2[j], p.uc1[j].out, o, s.g2, o, o, s.k2, s.d2, "up conv2")) return e;
     for (ConvLayer *c : {&p.uc1[j], &p.uc2[j]}) {
-      c->y_off = saved.take_floats(c->out.floats());
+      act_take(c->out.floats(), c->y_off);
       c->bn.coef_off = saved.take_floats((size_t)6 * c->bn.Cs);
       track_conv(p, *c);
     }
@@ -587,13 +600,21 @@ int build_plan(hcu_unet_plan &p) {
     const int pd[5] = {u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW};
     add_job(PREP_CONVT_DGRAD, prep_elems(u.dgrad), u.w_off, wpack_of(u.dgrad), pd, 5, u.wd_off);
   }
+  if (fwd_only) {
+    size_t mx = 1;
+    for (const auto &a : acts) mx = std::max(mx, a.second);
+    const size_t pp[2] = {saved.take_floats(mx), saved.take_floats(mx)};
+    for (size_t k = 0; k < acts.size(); ++k) *acts[k].first = pp[k & 1];
+  }
   p.saved_bytes = saved.off;
 
   Region scratch;
-  for (size_t &b : p.buf_off) b = scratch.take_floats(p.max_act);
+  // the gradient ring, the weight-gradient partials and the weight re-layout
+  // scratch are backward-only
+  for (size_t &b : p.buf_off) b = scratch.take_floats(fwd_only ? 0 : p.max_act);
   p.part_off = scratch.take_floats(p.max_part);
-  p.wpart_off = scratch.take_floats(p.max_part);
-  p.wprep_off = scratch.take_floats(p.max_wprep);
+  p.wpart_off = scratch.take_floats(fwd_only ? 0 : p.max_part);
+  p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
   p.scratch_bytes = scratch.off;
   return 0;
@@ -859,8 +880,15 @@ int hcu_version(void) { return 100; }
 
 int hcu_unet_plan_create(const hcu_unet_spec *spec, int B, int X, int Y, int Z,
                          hcu_unet_plan **out) {
+  return hcu_unet_plan_create_ex(spec, B, X, Y, Z, 0, out);
+}
+
+int hcu_unet_plan_create_ex(const hcu_unet_spec *spec, int B, int X, int Y, int Z, int flags,
+                            hcu_unet_plan **out) {
   if (!spec || !out) return fail(HCU_ERR_INVALID, "null argument");
+  if (flags & ~HCU_PLAN_FORWARD_ONLY) return fail(HCU_ERR_INVALID, "unknown plan flags");
   auto *p = new hcu_unet_plan();
+  p->flags = flags;
   p->spec = *spec;
   p->B = B;
   p->X = X;
@@ -1197,6 +1225,8 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
   if (!plan || !t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)
     return fail(HCU_ERR_INVALID, "null argument");
   const hcu_unet_plan &p = *plan;
+  if (p.flags & HCU_PLAN_FORWARD_ONLY)
+    return fail(HCU_ERR_INVALID, "backward through a forward-only plan (its activations are not kept)");
   std::vector<uintptr_t> key = {1, (uintptr_t)t->x, (uintptr_t)t->params, (uintptr_t)t->grads,
                                 (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)dout,
                                 (uintptr_t)dx, (uintptr_t)training, (uintptr_t)accumulate};

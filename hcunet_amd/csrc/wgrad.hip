@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
     tile /= a.ntz;
     const int tyi = tile % a.nty, txi = tile / a.nty;
     const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
-    __syncthreads();
+    lds_barrier();
     {  // stage A halo
       const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
       for (int idx = tid; idx < HAV * CA4; idx += 256) {
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
         dst[3 * PG] = val.w;
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (int ks = wave; ks < nks; ks += 4) {
       const int p = ks * 4 + (lane >> 4);
       const bool pv = p < PT;
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
   }
 
   // ---- cross-wave reduction in a fixed order, then one partial slab write
-  __syncthreads();
+  lds_barrier();
   float *red = smem;  // [MS*NS][64][4]
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WGradArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   const int nel = MS * NS * 256;
   for (int idx = tid; idx < nel; idx += 256) {
@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
 
   // zero everything once: padded z positions and unused rows stay finite (0)
   for (int i = tid; i < (nimg + 2) * PA + (CKG + 1) * PG; i += 256) smem[i] = 0.f;
-  __syncthreads();
+  lds_barrier();
   for (int i = tid; i < PA; i += 256) alds[(size_t)(nimg + 1) * PA + i] = 1.f;
   for (int q = tid; q < nks * 4; q += 256) {
     const int p = q * 4;
@@ -321,7 +321,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
     tile /= a.ntz;
     const int tyi = tile % a.nty, txi = tile / a.nty;
     const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
-    __syncthreads();
+    lds_barrier();
     // ---- A halo -> one channel-major image per kz shift (act applied, 0 outside)
     for (int base = tid; base < HAV * CA4; base += 4 * 256) {
       float4 val[4];
@@ -402,7 +402,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
         d[3 * PG] = val[u].w;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // ---- MFMA over the tile's voxels: wave w takes K-steps w, w+4, ...
     for (int ks = wave; ks < nks; ks += 4) {
       const int q = ks * 4 + g;
@@ -425,7 +425,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
   }
 
   // ---- cross-wave reduction in a fixed order, then one partial slab write
-  __syncthreads();
+  lds_barrier();
   float *red = smem;  // [MS*NS][64][4]
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
@@ -441,7 +441,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   const int kb = blockIdx.x;
   const int nel = MS * NS * 256;
@@ -690,7 +690,7 @@ __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize
     for (int k = sl; k < f.KB; k += S) acc += (double)src[(size_t)k * n];
   }
   red[tid] = acc;
-  __syncthreads();
+  lds_barrier();
   if (sl != 0 || idx >= n) return;
   double s = red[el];
   for (int j = 1; j < S; ++j) s += red[j * EPB + el];

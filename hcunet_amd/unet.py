@@ -138,7 +138,11 @@ class Unet_Constructor(nn.Module):
         bf16 = self._bf16()
         eng.check_input(x, bf16)
         params = eng.params_ready()
-        return _UnetFunction.apply(x, eng, bf16, *params)
+        # No gradient can flow (torch.no_grad(), or nothing requires grad): the
+        # forward-only plan, which keeps no activations for a backward.
+        fwd_only = not (torch.is_grad_enabled() and
+                        (x.requires_grad or any(p.requires_grad for p in params)))
+        return _UnetFunction.apply(x, eng, bf16, fwd_only, *params)
 
     # -- checkpointing (hcat/unet.py:145-196) --------------------------------
     def save(self, filename, hyperparameters=None):
@@ -328,10 +332,11 @@ def bn_modules(module):
 
 
 class _Plan:
-    def __init__(self, spec, B, X, Y, Z):
+    def __init__(self, spec, B, X, Y, Z, flags=0):
         L = _lib.lib()
         handle = ctypes.c_void_p()
-        _lib.check(L.hcu_unet_plan_create(ctypes.byref(spec), B, X, Y, Z, ctypes.byref(handle)),
+        _lib.check(L.hcu_unet_plan_create_ex(ctypes.byref(spec), B, X, Y, Z, flags,
+                                             ctypes.byref(handle)),
                    'Unet_Constructor')
         self.handle = handle
         out_shape = (ctypes.c_int64 * 5)()
@@ -385,14 +390,16 @@ class _Engine:
         if x.dtype not in ok:
             raise RuntimeError('Input type (%s) and weight type (float) should be the same' % x.dtype)
 
-    def plan(self, shape, bf16=False):
-        key = tuple(shape) + (bool(bf16),)
+    def plan(self, shape, bf16=False, forward_only=False):
+        """Launch plan for an input shape.  forward_only: the no-grad plan whose
+        forward keeps no activations for a backward (HCU_PLAN_FORWARD_ONLY)."""
+        key = tuple(shape) + (bool(bf16), bool(forward_only))
         p = self.plans.get(key)
         if p is None:
             B, _, X, Y, Z = tuple(shape)
             spec = _lib.UnetSpec.from_buffer_copy(self.spec)
             spec.compute_dtype = _lib.HCU_BF16 if bf16 else _lib.HCU_F32
-            p = _Plan(spec, B, X, Y, Z)
+            p = _Plan(spec, B, X, Y, Z, _lib.HCU_PLAN_FORWARD_ONLY if forward_only else 0)
             self.plans[key] = p
         return p
 
@@ -519,9 +526,9 @@ _X_DTYPES = {torch.float32: _lib.HCU_F32, torch.float16: _lib.HCU_F16,
 
 class _UnetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, eng, bf16, *params):
+    def forward(ctx, x, eng, bf16, fwd_only, *params):
         x = x.contiguous()
-        plan = eng.plan(x.shape, bf16)
+        plan = eng.plan(x.shape, bf16, forward_only=fwd_only)
         dev = x.device
         out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
         saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
@@ -540,7 +547,8 @@ class _UnetFunction(torch.autograd.Function):
         ctx.eng = eng
         ctx.plan = plan
         ctx.training = training
-        ctx.save_for_backward(x, saved)
+        if not fwd_only:
+            ctx.save_for_backward(x, saved)
         return out
 
     @staticmethod
@@ -567,4 +575,4 @@ class _UnetFunction(torch.autograd.Function):
         finish()
         if dx is not None and dx.dtype != x.dtype:
             dx = dx.to(x.dtype)
-        return (dx, None, None) + (None,) * len(eng.params)
+        return (dx, None, None, None) + (None,) * len(eng.params)

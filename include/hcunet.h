@@ -99,6 +99,17 @@ int hcu_unet_plan_create(const hcu_unet_spec *spec, int B, int X, int Y, int Z,
                          hcu_unet_plan **out);
 void hcu_unet_plan_destroy(hcu_unet_plan *plan);
 
+/* Plan flags.  HCU_PLAN_FORWARD_ONLY: inference (torch.no_grad) plan -- the
+ * forward keeps no activation for a backward (they alternate between two
+ * buffers of the largest activation), so saved_bytes is a small fraction of a
+ * training plan's; hcu_unet_backward on it fails with HCU_ERR_INVALID.
+ * Replaces the `with torch.no_grad(): unet(tile)` call of the reference's tiled
+ * inference loop (hcat/segment.py:82-99), which keeps autograd off but still
+ * runs the module's ordinary forward. */
+#define HCU_PLAN_FORWARD_ONLY 1
+int hcu_unet_plan_create_ex(const hcu_unet_spec *spec, int B, int X, int Y, int Z, int flags,
+                            hcu_unet_plan **out);
+
 /* out_shape[5] = output [B, out_channels, OX, OY, OZ]; n_params = number of
  * parameter scalars (flat layout = Unet_Constructor.parameters() order);
  * n_bn = number of BatchNorm3d modules; saved_bytes = forward->backward
@@ -214,6 +225,32 @@ int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy,
 /* nn.MaxPool3d(kernel=stride=k, floor mode) forward, channels-last. */
 int hcu_maxpool_fwd_cl(int B, int C, int X, int Y, int Z, const int *k,
                        const float *x, float *y, hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Tiled inference (hcat.segment.predict_segmentation_mask, hcat/segment.py:21-136;
+ * hcat.utils.pad_image_with_reflections / calculate_indexes, hcat/utils.py:33-124). */
+/* ------------------------------------------------------------------------ */
+#define HCU_TILE_BATCH_MAX 64
+/* out[b][c][i][j][k] = image[0][c][r(o_b + (i,j,k))] for n_tiles tiles of
+ * tile_dims, o_b = origins[3b..3b+2] in padded coordinates; r() is numpy's
+ * reflection padding (image[pad-1::-1], image, image[-1:-pad-1:-1]) with
+ * pad_lo[d] = min(pad, size) (pad_image_with_reflections, utils.py:51-71), and
+ * with clean != 0 values are cleaned as segment.py:66-67 does (NaN -> 0,
+ * +-Inf -> 1).
+ * image: [1][C][X][Y][Z] of image_dtype (HCU_F32 or HCU_F16), device memory;
+ * out: [n_tiles][C][tile_dims] fp32, the network input batch. */
+int hcu_tile_gather(const void *image, int image_dtype, int C, int X, int Y, int Z,
+                    const int *pad_lo, const int *origins, int n_tiles, const int *tile_dims,
+                    int clean, float *out, hcu_stream_t stream);
+/* mask[dst_lo + w] = f(out[crop_lo + w']) over the write box write_dims, with
+ * w' = w or 0 along dimensions where bcast[d] != 0 (torch broadcasting of a
+ * size-1 valid_out dimension, segment.py:121-123); out is one channel of one
+ * tile's network output [out_dims]; f = the in-place sigmoid chain of
+ * segment.py:110-113 (x*-1, exp, +1, pow(-1)), then 1/0 for f > thr when
+ * threshold != 0 (segment.py:116-119).  mask: [mask_dims] of HCU_F32 or HCU_U8. */
+int hcu_tile_scatter(const float *out, const int *out_dims, const int *crop_lo, const int *bcast,
+                     void *mask, int mask_dtype, const int *mask_dims, const int *dst_lo,
+                     const int *write_dims, int threshold, float thr, hcu_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Measurement: opt-in HIP-event timing of every library launch (bench.py). */
