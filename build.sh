@@ -5,14 +5,14 @@ set -euo pipefail
 cd "$(dirname "$0")"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 OUT=hcunet_amd/libhcunet.so
-SRC="hcunet_amd/csrc/timing.cpp hcunet_amd/csrc/gconv.hip hcunet_amd/csrc/conv2.hip hcunet_amd/csrc/conv8.hip hcunet_amd/csrc/wgrad.hip hcunet_amd/csrc/pointwise.hip hcunet_amd/csrc/loss_adam.hip hcunet_amd/csrc/prep_all.hip hcunet_amd/csrc/bconv.hip hcunet_amd/csrc/bwgrad.hip hcunet_amd/csrc/segment.hip hcunet_amd/csrc/unet.cpp"
+SRC="hcunet_amd/csrc/timing.cpp hcunet_amd/csrc/gconv.hip hcunet_amd/csrc/conv2.hip hcunet_amd/csrc/conv8.hip hcunet_amd/csrc/wgrad.hip hcunet_amd/csrc/pointwise.hip hcunet_amd/csrc/loss_adam.hip hcunet_amd/csrc/prep_all.hip hcunet_amd/csrc/bconv.hip hcunet_amd/csrc/bconv_f32.hip hcunet_amd/csrc/bwgrad.hip hcunet_amd/csrc/segment.hip hcunet_amd/csrc/unet.cpp"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude $*"
 mkdir -p build
 objs=()
 pids=()
 for s in $SRC; do
   o=build/$(basename "$s").o
-  if [ ! -f "$o" ] || [ "$s" -nt "$o" ] || [ hcunet_amd/csrc/common.h -nt "$o" ] || [ include/hcunet.h -nt "$o" ] || [ build.sh -nt "$o" ]; then
+  if [ ! -f "$o" ] || [ "$s" -nt "$o" ] || [ hcunet_amd/csrc/common.h -nt "$o" ] || [ hcunet_amd/csrc/bconv_kernel.h -nt "$o" ] || [ include/hcunet.h -nt "$o" ] || [ build.sh -nt "$o" ]; then
     lang=""
     case "$s" in *.cpp) lang="-x hip";; esac
     $HIPCC $lang $FLAGS -c "$s" -o "$o.tmp" && mv "$o.tmp" "$o" &

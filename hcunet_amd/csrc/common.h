@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <algorithm>
+#include <cstdlib>
 #include <string>
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -182,6 +184,7 @@ struct GConvArgs {
   // bconv (bconv.hip): the bf16 path.  in / out / bn_y / w point to bf16 data
   // (channels-last activations, packed weights); partial stays fp32.
   int use_bconv;
+  int bes;   // bconv element bytes: 2 (bf16 activations) or 4 (fp32); 0 = 2
 };
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
 // (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n
@@ -218,6 +221,22 @@ inline int plan_conv_any(GConvArgs &a, int target_blocks) {
   return plan_gconv(a, target_blocks);
 }
 int plan_bconv(GConvArgs &a, int target_blocks);
+// fp32 convolution: the blocked MFMA kernel (bconv, fp32 elements) when it
+// supports the shape, else conv8 / conv2 / the generic gconv.
+// HCU_NO_BCONV_F32=1 restores the older fp32 kernels (A/B testing).
+inline int plan_conv_fp32(GConvArgs &a, int target_blocks) {
+  static const bool off = getenv("HCU_NO_BCONV_F32") != nullptr;
+  // fewer than 16 output columns: conv8's 4x4 MFMA blocks waste no MFMA rows
+  if (!off && a.Cout * std::max(1, a.nph) >= 16) {
+    GConvArgs b = a;
+    b.bes = 4;
+    if (plan_bconv(b, target_blocks) == 0) {
+      a = b;
+      return 0;
+    }
+  }
+  return plan_conv_any(a, target_blocks);
+}
 int launch_bconv(const GConvArgs &a, hipStream_t s);
 int bconv_stat_rows(const GConvArgs &a);
 inline int launch_conv_any(const GConvArgs &a, hipStream_t s) {
@@ -374,6 +393,15 @@ struct WPack {
 };
 inline WPack wpack_of(const GConvArgs &a) {
   WPack p{};
+  if (a.use_bconv && a.bes == 4) {   // fp32 bconv: the conv2 image [chunk][s][g][co][4]
+    const int T = a.KX * a.KY * a.KZ, TPS = 16 / a.CK;
+    p.on = 1;
+    p.CK = a.CK;
+    p.S = (T + TPS - 1) / TPS;
+    p.ICs = a.ICs;
+    p.CoutW = a.CoutW;
+    return p;
+  }
   if (a.use_bconv) {   // bf16 image wg[chunk][s][g][co][8] (bconv.hip), 32 K per step
     const int T = a.KX * a.KY * a.KZ, TPS = 32 / a.CK;
     p.on = 3;
@@ -410,6 +438,7 @@ __host__ __device__ inline int64_t wpack_count(const WPack &p, int T, int ICs, i
 }
 inline size_t wprep_floats(const GConvArgs &a) {
   const int T = a.KX * a.KY * a.KZ;
+  if (a.use_bconv && a.bes == 4) return (size_t)wpack_count(wpack_of(a), T, a.ICs, a.CoutW);
   if (a.use_bconv) return (size_t)(wpack_count(wpack_of(a), T, a.ICs, a.CoutW) + 1) / 2;
   if (a.use_conv8) return (size_t)T * a.ICs * 8;
   if (!a.use_conv2) return (size_t)T * a.ICs * a.CoutW;

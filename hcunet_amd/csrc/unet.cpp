@@ -192,9 +192,9 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
   L.out = mkdims(in.B, ox, oy, oz, Cout, in.es);
   const bool bf = in.es == 2;
   L.fwd = gconv_conv_fwd(in, L.out, K, D, Cout);
-  if (int e = bf ? plan_bconv(L.fwd, kTargetBlocks) : plan_conv_any(L.fwd, kTargetBlocks)) return e;
+  if (int e = bf ? plan_bconv(L.fwd, kTargetBlocks) : plan_conv_fp32(L.fwd, kTargetBlocks)) return e;
   L.dgrad = gconv_conv_dgrad(in, L.out, K, D, L.E);
-  if (int e = bf ? plan_bconv(L.dgrad, kTargetBlocks) : plan_conv_any(L.dgrad, kTargetBlocks))
+  if (int e = bf ? plan_bconv(L.dgrad, kTargetBlocks) : plan_conv_fp32(L.dgrad, kTargetBlocks))
     return e;
   L.wg = wgrad_conv(in, L.out, K, D);
   if (int e = bf ? plan_bwgrad(L.wg, kTargetBlocks) : plan_wgrad(L.wg, kTargetBlocks)) return e;
@@ -246,7 +246,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
       u.fwdf = a;
       max_wprep = std::max(max_wprep, wprep_floats(a));
       max_kpart = std::max(max_kpart, conv_partial_floats(a));
-    } else if (plan_conv2(a, kTargetBlocks) == 0) {
+    } else if (plan_conv_fp32(a, kTargetBlocks) == 0 && (a.use_bconv || a.use_conv2)) {
       u.fwdf = a;
       max_wprep = std::max(max_wprep, wprep_floats(a));
       max_kpart = std::max(max_kpart, conv_partial_floats(a));
@@ -288,7 +288,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     a.KX = u.K[0]; a.KY = u.K[1]; a.KZ = u.K[2];
     a.sx = u.S[0]; a.sy = u.S[1]; a.sz = u.S[2];
     a.dx = a.dy = a.dz = 1;
-    if (int e = bf ? plan_bconv(a, kTargetBlocks) : plan_conv_any(a, kTargetBlocks)) return e;
+    if (int e = bf ? plan_bconv(a, kTargetBlocks) : plan_conv_fp32(a, kTargetBlocks)) return e;
     u.dgrad = a;
     max_wprep = std::max(max_wprep, wprep_floats(a));
     max_part = std::max(max_part, (size_t)gconv_rows(a) * a.CoutW * 2);
@@ -1292,7 +1292,7 @@ int prep_one(int kind, const GConvArgs &a, const int *prm, int np, const float *
              hipStream_t s) {
   PrepJob j{};
   j.kind = kind;
-  j.bf16 = a.use_bconv ? 1 : 0;
+  j.bf16 = (a.use_bconv && a.bes != 4) ? 1 : 0;
   j.n = (int64_t)prep_elems(a);
   j.src = 0;
   j.dst = 0;

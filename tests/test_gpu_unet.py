@@ -210,8 +210,14 @@ def test_bn_cancellation_large_bias_shifted_input():
     x = x + np.float32(6.0)
     mask, pwl = _mask_pwl(_oshape(spec, state, x))
     m, opt, out, loss, ref32, p32, p64 = run_step(m, spec, state, x, mask, pwl)
-    err_out = (out.detach().cpu().double() - ref32['out'].double()).abs().max().item()
-    assert err_out <= 1e-4, err_out
+    # forward output against the fp64 oracle: here the reference's own fp32
+    # arithmetic is ~9e-5 from fp64 (|out| ~ 4), so the bar is the larger of
+    # 1e-4 and twice that fp32 noise
+    out64 = uo.OracleUnet(spec, state, dtype=torch.float64).forward(
+        torch.as_tensor(x).double(), training=True).detach()
+    noise = (ref32['out'].double() - out64).abs().max().item()
+    err_out = (out.detach().cpu().double() - out64).abs().max().item()
+    assert err_out <= max(1e-4, 2.0 * noise), (err_out, noise)
     check_grads(m, spec, p32, p64)
     check_running_stats(m, spec, ref32)
 

@@ -7,9 +7,11 @@
 //     MODE f = forward (+ BatchNorm statistics rows), d = input gradient
 //     (padding K-1), db = input gradient with the fused BatchNorm backward
 //     epilogue; ACT 1 = BatchNorm+ReLU applied to the input while staging.
-//   HCU_BCONV_FORCE="CK,NSUB,MPW[,NPF]" pins the tiling.
+//   HCU_BCONV_FORCE="CK,NSUB,MPW[,NPF]" pins the tiling; BCONV_ES=4 runs the
+//   fp32 kernels (default 2: bf16).
 #define HCU_BCONV_PHASES 1
 #include "../hcunet_amd/csrc/bconv.hip"
+#include "../hcunet_amd/csrc/bconv_f32.hip"
 
 #include <chrono>
 #include <cstring>
@@ -64,6 +66,9 @@ int main(int argc, char **argv) {
   const bool bnbwd = mode == "db";
 
   GConvArgs a{};
+  const char *es_env = getenv("BCONV_ES");
+  a.bes = es_env ? atoi(es_env) : 2;
+  const int ES = a.bes;
   a.B = B;
   a.IX = IX; a.IY = IY; a.IZ = IZ; a.ICs = ICs;
   if (dgrad) {
@@ -84,23 +89,34 @@ int main(int argc, char **argv) {
     return 1;
   }
   const int T = K[0] * K[1] * K[2];
-  const int TPS = 32 / a.CK;
+  const int TPS = (ES == 2 ? 32 : 16) / a.CK;
   const int S = (T + TPS - 1) / TPS;
   const size_t n_in = (size_t)B * IX * IY * IZ * ICs;
   const size_t n_out = (size_t)B * a.SX * a.SY * a.SZ * a.OCs;
-  const size_t n_w = (size_t)(ICs / a.CK) * S * 4 * a.CoutW * 8;
+  const size_t n_w = (size_t)(ICs / a.CK) * S * 4 * a.CoutW * (16 / ES);
   std::mt19937 rng(1);
   std::uniform_real_distribution<float> U(-1.f, 1.f);
-  std::vector<uint16_t> hin(n_in), hw(n_w), hy(n_out);
-  for (auto &v : hin) v = to_bf(U(rng));
-  for (auto &v : hw) v = to_bf(0.05f * U(rng));
-  for (auto &v : hy) v = to_bf(U(rng));
+  // element images as 16-bit words (bf16, or two halves of an fp32)
+  std::vector<uint16_t> hin(n_in * ES / 2), hw(n_w * ES / 2), hy(n_out * ES / 2);
+  auto fill = [&](std::vector<uint16_t> &h, float sc) {
+    if (ES == 2) {
+      for (auto &v : h) v = to_bf(sc * U(rng));
+    } else {
+      for (size_t i = 0; i < h.size(); i += 2) {
+        const float f = sc * U(rng);
+        memcpy(&h[i], &f, 4);
+      }
+    }
+  };
+  fill(hin, 1.f);
+  fill(hw, 0.05f);
+  fill(hy, 1.f);
   std::vector<float> hsc(ICs, 1.1f), hsh(ICs, 0.05f), hb(Cout, 0.01f), hco(a.OCs, 0.5f);
   std::vector<uint16_t> none;
-  a.in = reinterpret_cast<const float *>(dev_fill(n_in, hin));
-  a.w = reinterpret_cast<const float *>(dev_fill(n_w, hw));
+  a.in = reinterpret_cast<const float *>(dev_fill(hin.size(), hin));
+  a.w = reinterpret_cast<const float *>(dev_fill(hw.size(), hw));
   uint16_t *dout = nullptr;
-  CK_HIP(hipMalloc(&dout, n_out * 2));
+  CK_HIP(hipMalloc(&dout, n_out * ES));
   a.out = reinterpret_cast<float *>(dout);
   a.bias = dev_fill((size_t)Cout, hb);
   if (act) {
@@ -108,7 +124,7 @@ int main(int argc, char **argv) {
     a.in_shift = dev_fill((size_t)ICs, hsh);
   }
   if (bnbwd) {
-    a.bn_y = reinterpret_cast<const float *>(dev_fill(n_out, hy));
+    a.bn_y = reinterpret_cast<const float *>(dev_fill(hy.size(), hy));
     a.bn_scale = dev_fill((size_t)a.OCs, hco);
     a.bn_shift = dev_fill((size_t)a.OCs, hco);
     a.bn_mean = dev_fill((size_t)a.OCs, hco);
@@ -140,10 +156,10 @@ int main(int argc, char **argv) {
   CK_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_bconv_phase), sizeof(ph)));
   const double us = ms * 1e3 / iters;
   const double flops = 2.0 * B * a.OX * a.OY * a.OZ * (double)Cout * T * ICs;
-  const double bytes = 2.0 * (n_in + n_out) + (bnbwd ? 2.0 * n_out : 0.0);
-  printf("%s B%d I%dx%dx%d ICs%d Cout%d K%dx%dx%d act%d | CK%d NSUB%d MPW%d T%dx%dx%d NPF%d ks%d grid%d "
+  const double bytes = (double)ES * (n_in + n_out) + (bnbwd ? (double)ES * n_out : 0.0);
+  printf("es%d %s B%d I%dx%dx%d ICs%d Cout%d K%dx%dx%d act%d | CK%d NSUB%d MPW%d T%dx%dx%d NPF%d ks%d grid%d "
          "lds%d | %.1f us  %.1f TF/s  %.0f GB/s\n",
-         mode.c_str(), B, IX, IY, IZ, ICs, Cout, K[0], K[1], K[2], act, a.CK, a.NSUB, a.MPW, a.TX,
+         ES, mode.c_str(), B, IX, IY, IZ, ICs, Cout, K[0], K[1], K[2], act, a.CK, a.NSUB, a.MPW, a.TX,
          a.TY, a.TZ, a.NPF, a.ksplit, a.gridx, a.lds_bytes, us, flops / us * 1e-6,
          bytes / us * 1e-3);
   double tot = 0;
