@@ -42,10 +42,19 @@ bool conv8_disabled() {   // HCU_NO_CONV8=1 keeps the 16x16x4 kernels (A/B testi
   return off;
 }
 
-template <int C4, int G, int NPF>
+// BNB: input gradient with the fused BatchNorm backward (a.bn_y set); a
+// template parameter so its loads never share registers or waits with the
+// forward epilogue.  Launch constants used in the tile loop are read from an
+// LDS copy of the arguments (kuni, common.h), so they do not pin scalar
+// registers for the whole kernel.
+template <int C4, int G, int NPF, bool BNB>
 __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ __attribute__((aligned(16))) char sa_raw[sizeof(GConvArgs)];
+  GConvArgs &sa = *reinterpret_cast<GConvArgs *>(sa_raw);
+#define KA(f) kuni(sa.f)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) sa = a;
   const int T = a.KX * a.KY * a.KZ;
   const int HZ = a.HZ, HYZ = a.HY * a.HZ, HV = a.HX * HYZ, HVP = a.HVP;
   const int MT = a.TX * a.TY * a.MZ;   // M rows: z stride MZ (>= TZ; rows with lz >= TZ are idle)
@@ -89,33 +98,24 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   const int col = ((lane >> 5) << 2) | (lane & 3);
   const int wcol = col * 4;
   const bool cstore = col < a.OCs, cstat = col < a.Cout;
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)a.out, 0, a.B * a.SX * a.SY * a.SZ * a.OCs * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)a.bn_y, 0, a.bn_y ? a.B * a.SX * a.SY * a.SZ * a.OCs * 4 : 0, 0x00020000);
-  const float bnsc = (a.bn_y && cstat) ? a.bn_scale[col] : 0.f;
-  const float bnsh = (a.bn_y && cstat) ? a.bn_shift[col] : 0.f;
-  const float bnmu = (a.bn_y && cstat) ? a.bn_mean[col] : 0.f;
-  const float bnis = (a.bn_y && cstat) ? a.bn_invstd[col] : 0.f;
+  const float bnsc = (BNB && cstat) ? a.bn_scale[col] : 0.f;
+  const float bnsh = (BNB && cstat) ? a.bn_shift[col] : 0.f;
+  const float bnmu = (BNB && cstat) ? a.bn_mean[col] : 0.f;
+  const float bnis = (BNB && cstat) ? a.bn_invstd[col] : 0.f;
   const float bias = (a.bias && cstat) ? a.bias[col] : 0.f;
   // forward statistics about a block-wide pivot per channel (the value of the
   // block's first output voxel; StatRow in common.h)
-  const bool fwdstat = a.stats && !a.bn_y;
+  const bool fwdstat = a.stats && !BNB;
   float s1 = 0.f, s2 = 0.f, cnt = 0.f, piv = 0.f;
   bool have_piv = false;
   const bool act = a.in_scale != nullptr;
   const int S = T * C4;
 
-  // Tap offsets are wave-uniform scalar arithmetic (no LDS read in the address
-  // chain, so waiting for a step's fragments never drains the next step's).
-  const int tdx = a.dx * HYZ * 4, tdy = a.dy * HZ * 4, tdz = a.dz * 4;
+  // Tap offsets come from the LDS table (toffs, float offsets per tap).
   auto load = [&](int s, floatx4 &bw, floatx4 (&av)[G]) {
     const int t = s / C4, q = s - t * C4;
-    int t1, kz, kx, ky;
-    a.fKZ.divmod(t, t1, kz);
-    a.fKY.divmod(t1, kx, ky);
     bw = *reinterpret_cast<const floatx4 *>(wlds + s * 32 + wcol);
-    const float *ap = alds + (size_t)q * HVP * 4 + kx * tdx + ky * tdy + kz * tdz;
+    const float *ap = alds + (size_t)q * HVP * 4 + toffs[t];
 #pragma unroll
     for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const floatx4 *>(ap + vb[g]);
   };
@@ -146,22 +146,27 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   // element outside the input gets an out-of-range offset, which the hardware
   // range check turns into 0 (no branch per element); BatchNorm+ReLU is
   // applied when the element is written to LDS, selected to 0 outside.
-  const uint32_t bX = (uint32_t)a.IY * a.IZ * a.ICs * 4, bY = (uint32_t)a.IZ * a.ICs * 4,
-                 bZ = (uint32_t)a.ICs * 4;
-  const int sample_bytes = a.IX * a.IY * a.IZ * a.ICs * 4;
   floatx4 pf[NPF];
   uint32_t okbits = 0;
+  auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
+    int r, tzi, tyi, txi;
+    sa.fNT.uni().divmod(tile, b, r);
+    sa.fNTZ.uni().divmod(r, r, tzi);
+    sa.fNTY.uni().divmod(r, txi, tyi);
+    ox0 = txi * KA(TX);
+    oy0 = tyi * KA(TY);
+    oz0 = tzi * KA(TZ);
+  };
+  // branch-free: invalid elements read an offset past the buffer (-> 0)
   auto fetch = [&](int tile) {
-    int b, r, tzi, tyi, txi;
-    a.fNT.divmod(tile, b, r);
-    a.fNTZ.divmod(r, r, tzi);
-    a.fNTY.divmod(r, txi, tyi);
-    const int gx0 = txi * a.TX - a.px, gy0 = tyi * a.TY - a.py, gz0 = tzi * a.TZ - a.pz;
-    const bool inb = gx0 >= 0 && gy0 >= 0 && gz0 >= 0 && gx0 + a.HX <= a.IX &&
-                     gy0 + a.HY <= a.IY && gz0 + a.HZr <= a.IZ;
-    const float *bp = a.in + (size_t)b * a.IX * a.IY * a.IZ * a.ICs;
+    int b, ox0, oy0, oz0;
+    tile_origin(tile, b, ox0, oy0, oz0);
+    const int IX = KA(IX), IY = KA(IY), IZ = KA(IZ), ICs = KA(ICs), HZr = KA(HZr);
+    const uint32_t bZ = (uint32_t)ICs * 4, bY = (uint32_t)IZ * bZ, bX = (uint32_t)IY * bY;
+    const int gx0 = ox0 - KA(px), gy0 = oy0 - KA(py), gz0 = oz0 - KA(pz);
+    const float *bp = KA(in) + (size_t)b * IX * bX / 4;
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, (a.dbg & 2) ? 0 : sample_bytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, IX * (int)bX, 0x00020000);
     const int base_off = gx0 * (int)bX + gy0 * (int)bY + gz0 * (int)bZ + cq * 4;
     okbits = 0;
 #pragma unroll
@@ -169,27 +174,33 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       const int hp = hpk[u];
       const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
       const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
-      const bool ok = hp >= 0 && hz < a.HZr && (inb || ((unsigned)gx < (unsigned)a.IX &&
-                                          (unsigned)gy < (unsigned)a.IY &&
-                                          (unsigned)gz < (unsigned)a.IZ));
+      const bool ok = (hp >= 0) & (hz < HZr) & ((unsigned)gx < (unsigned)IX) &
+                      ((unsigned)gy < (unsigned)IY) & ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
       pf[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      okbits |= (ok ? 1u : 0u) << u;
+      okbits |= (uint32_t)ok << u;
     }
   };
+  // The epilogue issues 4*G stores after the next tile's halo loads; where the
+  // path into the halo wait has no epilogue (the first tile) as many stores go
+  // to an empty buffer (dropped), so the compiler's wait for each prefetched
+  // element never includes output stores.
+  auto dummy_epilogue = [&]() {
+    const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, 0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 4 * G; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, zr, 64 * k, 0, 0);
+  };
+  lds_barrier();   // sa and the tables are in LDS
   // contiguous tile range per block (consecutive tiles share halo rows in L2)
   const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
   const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
   if (t_beg < t_end) fetch(t_beg);
-  if (a.dbg & 32) return;
+  dummy_epilogue();
 
   for (int tile = t_beg; tile < t_end; ++tile) {
-    int b, r, tzi, tyi, txi;
-    a.fNT.divmod(tile, b, r);
-    a.fNTZ.divmod(r, r, tzi);
-    a.fNTY.divmod(r, txi, tyi);
-    const int ox0 = txi * a.TX, oy0 = tyi * a.TY, oz0 = tzi * a.TZ;
+    int b, ox0, oy0, oz0;
+    tile_origin(tile, b, ox0, oy0, oz0);
     lds_barrier();
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
@@ -205,7 +216,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       // elements past the halo write the unused last slot of the last plane
       const int slot = hpk[u] >= 0 ? (idx % C4) * HVP + idx / C4 : C4 * HVP - 1;
-      if (!(a.dbg & 16)) *reinterpret_cast<floatx4 *>(alds + (size_t)slot * 4) = ok ? v : z;
+      *reinterpret_cast<floatx4 *>(alds + (size_t)slot * 4) = ok ? v : z;
     }
     lds_barrier();
     if (tile + 1 < t_end) fetch(tile + 1);
@@ -215,7 +226,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     for (int g = 0; g < G; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
     floatx4 b0, b1, a0[G], a1[G];
     load(0, b0, a0);
-    for (int s = 0; s < ((a.dbg & 1) ? 0 : S); s += 2) {
+    for (int s = 0; s < S; s += 2) {
       load(min(s + 1, S - 1), b1, a1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -237,8 +248,16 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     // offsets are read from LDS up front (one wait), and the output pointer is
     // a global-address-space pointer so the stores cannot alias LDS and do not
     // serialise the table reads.
-    const int tbase = ((((b * a.SX + ox0) * a.SY + oy0) * a.SZ + oz0) * a.OCs + col) * 4;
-    const bool interior = ox0 + a.TX <= a.OX && oy0 + a.TY <= a.OY && oz0 + a.TZ <= a.OZ;
+    const int OX = KA(OX), OY = KA(OY), OZ = KA(OZ), OCs = KA(OCs), SY = KA(SY), SZ = KA(SZ);
+    const int sample = KA(SX) * SY * SZ * OCs;
+    // per-sample buffers (32-bit offsets within one sample)
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(KA(out) + (size_t)b * sample), 0, sample * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        BNB ? (void *)(KA(bn_y) + (size_t)b * sample) : (void *)a.in, 0, BNB ? sample * 4 : 0,
+        0x00020000);
+    const int tbase = (((ox0 * SY + oy0) * SZ + oz0) * OCs + col) * 4;
+    const bool interior = ox0 + KA(TX) <= OX && oy0 + KA(TY) <= OY && oz0 + KA(TZ) <= OZ;
     int ro[G * 4];
     const int mb = wave * G * 32 + ((lane >> 2) & 7) * 4;
 #pragma unroll
@@ -251,8 +270,8 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int pk = rowpk[mb + g * 32 + rr];
-          const bool in = ox0 + (pk >> 20) < a.OX && oy0 + ((pk >> 10) & 1023) < a.OY &&
-                          oz0 + (pk & 1023) < a.OZ;
+          const bool in = (ox0 + (pk >> 20) < OX) & (oy0 + ((pk >> 10) & 1023) < OY) &
+                          (oz0 + (pk & 1023) < OZ);
           ro[g * 4 + rr] = in ? ro[g * 4 + rr] : -1;
         }
     }
@@ -263,13 +282,13 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       have_piv = true;
     }
 #pragma unroll
-    for (int g = 0; g < ((a.dbg & 8) ? 0 : G); ++g) {
+    for (int g = 0; g < G; ++g) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int o = ro[g * 4 + rr];
         float v = acc[g][rr] + bias;
         float w2 = v - piv, w1 = v - piv;
-        if (a.bn_y) {   // fused BatchNorm+ReLU backward: v = dA -> dz, stats (dz, dz*xhat)
+        if (BNB) {   // fused BatchNorm+ReLU backward: v = dA -> dz, stats (dz, dz*xhat)
           const float yv = __builtin_bit_cast(
               float, __builtin_amdgcn_raw_buffer_load_b32(yrs, o >= 0 ? tbase + o * 4 : 0x7ffffff0, 0, 0));
           v = fmaf(yv, bnsc, bnsh) > 0.f ? v : 0.f;
@@ -278,7 +297,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
         }
         __builtin_amdgcn_raw_buffer_store_b32(
             __builtin_bit_cast(uint32_t, v), ors,
-            (o >= 0 && cstore && !(a.dbg & 4)) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
+            (o >= 0 && cstore) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
         const bool ok = o >= 0 && cstat;
         const float w = ok ? w1 : 0.f;
         s1 += w;
@@ -322,12 +341,14 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       a.stats[((size_t)blockIdx.x * 8 + tid) * 2 + 1] = t2;
     }
   }
+#undef KA
 }
 
 // ---------------------------------------------------------------------------
 static long conv8_lds(const GConvArgs &a, int C4, int HVP, int G) {
   const int T = a.KX * a.KY * a.KZ;
-  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G + 8) * 4;
+  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G + 8) * 4 +
+         (long)sizeof(GConvArgs);   // + the static copy of the arguments
 }
 
 // Chooses the tile, groups per wave and grid for conv8_kernel; non-zero when
@@ -363,7 +384,8 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
     const int HVP = round_up(HV, 16) + 8;
     const long lds = conv8_lds(a, C4, HVP, G);
     const long tiles = (long)a.B * cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz;
-    if (lds > 80 * 1024 || HV * C4 > 16 * 256) continue;
+    // <= 12 prefetched elements per thread (16 spills registers at G = 8)
+    if (lds > 80 * 1024 || HV * C4 > 12 * 256) continue;
     a.G8 = G;
     a.TX = TX;
     a.TY = TY;
@@ -398,10 +420,6 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   a.fNTZ = FastDiv(a.ntz);
   a.fNTY = FastDiv(a.nty);
   a.fKZ = FastDiv(a.KZ);
-  {
-    const char *e = getenv("HCU_CONV8_DBG");
-    a.dbg = e ? atoi(e) : 0;
-  }
   a.fKY = FastDiv(a.KY);
   const long tiles = (long)a.B * a.ntx * a.nty * a.ntz;
   const int occ = std::max(1, std::min(4, (int)(160 * 1024 / a.lds_bytes)));
@@ -411,12 +429,17 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   return 0;
 }
 
-#define CONV8_CASE(C4_, G_, NPF_)                                                               \
-  if (C4 == C4_ && a.G8 == G_ && a.NPF == NPF_) {                                               \
-    HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ">", fl, by,                            \
-              hipLaunchKernelGGL((conv8_kernel<C4_, G_, NPF_>), dim3(a.gridx), dim3(256),       \
-                                 a.lds_bytes, s, a));                                           \
-    launched = true;                                                                            \
+#define CONV8_CASE(C4_, G_, NPF_)                                                                \
+  if (C4 == C4_ && a.G8 == G_ && a.NPF == NPF_) {                                                \
+    if (a.bn_y)                                                                                  \
+      HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ",bnb>", fl, by,                       \
+                hipLaunchKernelGGL((conv8_kernel<C4_, G_, NPF_, true>), dim3(a.gridx), dim3(256), \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
+    else                                                                                         \
+      HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ">", fl, by,                           \
+                hipLaunchKernelGGL((conv8_kernel<C4_, G_, NPF_, false>), dim3(a.gridx), dim3(256), \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
+    launched = true;                                                                             \
   }
 #define CONV8_NPF(C4_, G_) \
   CONV8_CASE(C4_, G_, 8) else CONV8_CASE(C4_, G_, 12) else CONV8_CASE(C4_, G_, 16)

@@ -204,23 +204,24 @@ int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, int W, doubl
 
 // ---------------------------------------------------------------------------
 // MaxPool3d forward on relu(bn(y)), kernel == stride, floor mode.
+// Index decomposition (window, channel quad) -> (b, px, py, pz, c4) with
+// magic-number divisions on 32-bit indices (the launcher checks the range):
+// 64-bit division is a ~100-instruction software sequence per element.
+struct PoolDiv {
+  FastDiv c4, pz, py, px;
+};
 template <typename T>
 __global__ void __launch_bounds__(256)
 maxpool_fwd_kernel(const T *y, const float *scale, const float *shift, T *p,
                    int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
-                   int PX, int PY, int PZ) {
-  const int C4 = Cs / 4;
-  const int64_t n = (int64_t)B * PX * PY * PZ * C4;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < n;
-       idx += (int64_t)gridDim.x * 256) {
-    const int c4 = (int)(idx % C4);
-    int64_t v = idx / C4;
-    const int pz = (int)(v % PZ);
-    v /= PZ;
-    const int py = (int)(v % PY);
-    v /= PY;
-    const int px = (int)(v % PX);
-    const int b = (int)(v / PX);
+                   int PX, int PY, int PZ, PoolDiv dv) {
+  const uint32_t n = (uint32_t)B * PX * PY * PZ * (Cs / 4);
+  for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < n; idx += gridDim.x * 256) {
+    int v, c4, pz, py, px, b;
+    dv.c4.divmod(idx, v, c4);
+    dv.pz.divmod((uint32_t)v, v, pz);
+    dv.py.divmod((uint32_t)v, v, py);
+    dv.px.divmod((uint32_t)v, b, px);
     const int c = c4 * 4;
     float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
     if (scale) {
@@ -255,15 +256,25 @@ static int grid_for(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
 }
 
+static PoolDiv pool_div(int Cs, int PX, int PY, int PZ) {
+  PoolDiv d;
+  d.c4 = FastDiv(Cs / 4);
+  d.pz = FastDiv(PZ);
+  d.py = FastDiv(PY);
+  d.px = FastDiv(PX);
+  return d;
+}
+
 int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
                        float *p, int B, int X, int Y, int Z, int Cs, int kx, int ky,
                        int kz, hipStream_t s, int bf) {
   const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
   const int64_t n = (int64_t)B * PX * PY * PZ * (Cs / 4);
+  if (n >= (int64_t)1 << 31) return fail(4, "max_pool3d: more than 2^31 channel quads per launch");
   HCU_TIMED(s, "maxpool_fwd_kernel", 0.0, 0.0,
             HCU_BF_DISPATCH(bf, maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s,
                             (const T *)y, scale, shift, (T *)p, B, X, Y, Z, Cs, kx, ky, kz, PX,
-                            PY, PZ));
+                            PY, PZ, pool_div(Cs, PX, PY, PZ)));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -326,9 +337,9 @@ bn_bwd_reduce_dense_kernel(T *dA, const T *y, BNCoef coef, int64_t nvox,
     const int c = (int)((beg + tid) % C4) * 4;
     const float4 sc = ld4(coef.scale + c), sh = ld4(coef.shift + c);
     const float4 mu = ld4(coef.mean + c), is = ld4(coef.invstd + c);
+    // e = vox * C4 + c / 4 with c fixed per thread: off = e * 4 exactly
     for (int64_t e = beg + tid; e < end; e += g.tb) {
-      const int64_t vox = e / C4;
-      const size_t off = (size_t)vox * Cs + c;
+      const size_t off = (size_t)e * 4;
       const float4 yy = ld4(y + off);
       float4 d = ld4(dA + off);
       d.x = fmaf(yy.x, sc.x, sh.x) > 0.f ? d.x : 0.f;
@@ -370,7 +381,7 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 bn_bwd_reduce_pool_kernel(const T *dP, const T *y, BNCoef coef, T *dz,
                           int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz,
-                          float *part, RedGeom g) {
+                          float *part, RedGeom g, PoolDiv dv) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int C4 = Cs / 4, tid = threadIdx.x;
   const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
@@ -382,13 +393,11 @@ bn_bwd_reduce_pool_kernel(const T *dP, const T *y, BNCoef coef, T *dz,
     const float4 sc = ld4(coef.scale + c), sh = ld4(coef.shift + c);
     const float4 mu = ld4(coef.mean + c), is = ld4(coef.invstd + c);
     for (int64_t e = beg + tid; e < end; e += g.tb) {
-      int64_t w = e / C4;
-      const int wz = (int)(w % PZ);
-      w /= PZ;
-      const int wy = (int)(w % PY);
-      w /= PY;
-      const int wx = (int)(w % PX);
-      const int b = (int)(w / PX);
+      int w, c4, wz, wy, wx, b;
+      dv.c4.divmod((uint32_t)e, w, c4);
+      dv.pz.divmod((uint32_t)w, w, wz);
+      dv.py.divmod((uint32_t)w, w, wy);
+      dv.px.divmod((uint32_t)w, b, wx);
       const int x0 = wx * kx, y0 = wy * ky, z0 = wz * kz;
       const int x1 = wx == PX - 1 ? X : x0 + kx, y1 = wy == PY - 1 ? Y : y0 + ky,
                 z1 = wz == PZ - 1 ? Z : z0 + kz;
@@ -447,37 +456,60 @@ int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, floa
                               int B, int X, int Y, int Z, int Cs, int kx, int ky,
                               int kz, float *part, int R, hipStream_t s, int bf) {
   const RedGeom g = red_geom((int64_t)B * (X / kx) * (Y / ky) * (Z / kz), Cs, R);
+  if (g.total >= (int64_t)1 << 31) return fail(4, "max_pool3d backward: more than 2^31 channel quads");
   HCU_TIMED(s, "bn_bwd_reduce_pool_kernel", 0.0, 0.0,
             HCU_BF_DISPATCH(bf, bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
                             (size_t)std::max(g.tb, 256) * 8 * 4, s, (const T *)dP, (const T *)y,
-                            coef, (T *)dz, B, X, Y, Z, Cs, kx, ky, kz, part, g));
+                            coef, (T *)dz, B, X, Y, Z, Cs, kx, ky, kz, part, g,
+                            pool_div(Cs, X / kx, Y / ky, Z / kz)));
   HCU_CHECK_LAUNCH();
   return 0;
 }
 
 // dy = dz*scale + c1*y + c0, in place.
+// The launcher makes the grid stride a multiple of C4, so each thread's channel
+// quad (and its coefficients) is fixed; 4 independent quads per iteration keep
+// 8 loads in flight per thread.
 template <typename T>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_kernel(T *dz, const T *y, BNCoef coef, int64_t n4, int C4) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * 256) {
-    const int c = (int)(i % C4) * 4;
-    const float4 sc = ld4(coef.scale + c), c1 = ld4(coef.c1 + c), c0 = ld4(coef.c0 + c);
-    const float4 yy = ld4(y + i * 4);
-    float4 d = ld4(dz + i * 4);
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t st = (int64_t)gridDim.x * 256;
+  const int c = (int)(i0 % C4) * 4;
+  const float4 sc = ld4(coef.scale + c), c1 = ld4(coef.c1 + c), c0 = ld4(coef.c0 + c);
+  auto f = [&](float4 d, float4 yy) {
     d.x = fmaf(d.x, sc.x, fmaf(c1.x, yy.x, c0.x));
     d.y = fmaf(d.y, sc.y, fmaf(c1.y, yy.y, c0.y));
     d.z = fmaf(d.z, sc.z, fmaf(c1.z, yy.z, c0.z));
     d.w = fmaf(d.w, sc.w, fmaf(c1.w, yy.w, c0.w));
-    st4(dz + i * 4, d);
+    return d;
+  };
+  int64_t i = i0;
+  for (; i + 3 * st < n4; i += 4 * st) {
+    float4 yy[4], d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      yy[u] = ld4(y + (i + u * st) * 4);
+      d[u] = ld4(dz + (i + u * st) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st4(dz + (i + u * st) * 4, f(d[u], yy[u]));
   }
+  for (; i < n4; i += st) st4(dz + i * 4, f(ld4(dz + i * 4), ld4(y + i * 4)));
 }
 
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, int Cs,
                         hipStream_t s, int bf) {
   const int64_t n4 = nvox * (Cs / 4);
+  const int C4 = Cs / 4;
+  // grid * 256 must be a multiple of C4 (fixed channel quad per thread)
+  int grid = grid_for(n4);
+  if (256 % C4) {
+    const int per = C4 / std::__gcd(256, C4);   // blocks per period
+    grid = std::max(per, grid / per * per);
+  }
   HCU_TIMED(s, "bn_bwd_apply_kernel", 0.0, 0.0,
-            HCU_BF_DISPATCH(bf, bn_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, s,
+            HCU_BF_DISPATCH(bf, bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, s,
                             (T *)dz, (const T *)y, coef, n4, Cs / 4));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -676,15 +708,12 @@ int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
 // ---------------------------------------------------------------------------
 template <typename TI, typename T>
 __global__ void __launch_bounds__(256)
-to_cl_kernel(const TI *x, T *xcl, int B, int C, int Cs, int64_t V) {
-  const int C4 = Cs / 4;
-  const int64_t n = (int64_t)B * C4 * V;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * 256) {
-    const int64_t v = i % V;
-    const int64_t q = i / V;
-    const int c4 = (int)(q % C4);
-    const int b = (int)(q / C4);
+to_cl_kernel(const TI *x, T *xcl, int B, int C, int Cs, int64_t V, FastDiv fV, FastDiv fC4) {
+  const uint32_t n = (uint32_t)(B * (Cs / 4) * V);   // < 2^31 (launcher)
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    int q, v, b, c4;
+    fV.divmod(i, q, v);
+    fC4.divmod((uint32_t)q, b, c4);
     float r[4];
     for (int j = 0; j < 4; ++j) {
       const int c = c4 * 4 + j;
@@ -698,27 +727,29 @@ to_cl_kernel(const TI *x, T *xcl, int B, int C, int Cs, int64_t V) {
 int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s,
                  int bf, int x_dtype) {
   const int64_t n = (int64_t)B * (Cs / 4) * V;
+  if (n >= (int64_t)1 << 31) return fail(4, "input volume: more than 2^31 channel quads");
   const dim3 gr(grid_for(n));
+  const FastDiv fV((uint32_t)V), fC4((uint32_t)(Cs / 4));
   if (x_dtype == 1 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<_Float16, bf16_t>), gr, dim3(256), 0, s,
-                                 (const _Float16 *)x, (bf16_t *)xcl, B, C, Cs, V));
+                                 (const _Float16 *)x, (bf16_t *)xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 3 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<bf16_t, bf16_t>), gr, dim3(256), 0, s,
-                                 (const bf16_t *)x, (bf16_t *)xcl, B, C, Cs, V));
+                                 (const bf16_t *)x, (bf16_t *)xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 0 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<float, bf16_t>), gr, dim3(256), 0, s, x,
-                                 (bf16_t *)xcl, B, C, Cs, V));
+                                 (bf16_t *)xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 1)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<_Float16, float>), gr, dim3(256), 0, s,
-                                 (const _Float16 *)x, xcl, B, C, Cs, V));
+                                 (const _Float16 *)x, xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 0)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<float, float>), gr, dim3(256), 0, s, x, xcl, B, C,
-                                 Cs, V));
+                                 Cs, V, fV, fC4));
   else
     return fail(4, "to_cl: unsupported input dtype");
   HCU_CHECK_LAUNCH();
