@@ -294,10 +294,17 @@ struct WGradArgs {
   // are the LDS row strides of the A halo / G images, MSW the row subtiles per
   // wave, NSB the column subtiles of a block.
   int use_bw, MSW, NSB, PTV, HAV, HGV;
+  // wgrad8 (wgrad8.hip, v2 == 2): A image z-row stride (PA2 / PG2: plane
+  // strides), MFMA form (0: 16x16x4, 1: 4x4x1 16-block), voxel blocks per
+  // instruction and z taps on the column side (form 1)
+  int ARS, w8mode, w8nbv, w8nj, w8nh, w8dbg;
+  int w8off[128];                     // wgrad8 row (form 0) / row-quad (form 1) A image offsets
 };
 int plan_bwgrad(WGradArgs &a, int target_blocks);
 int launch_bwgrad(const WGradArgs &a, hipStream_t s);
 int plan_wgrad(WGradArgs &a, int target_blocks);
+int plan_wgrad8(WGradArgs &a);
+int launch_wgrad8(const WGradArgs &a, hipStream_t s);
 int launch_wgrad(const WGradArgs &a, hipStream_t s);
 inline size_t wgrad_partial_floats(const WGradArgs &a) {
   return (size_t)a.KB * a.Mtot * a.Ntot;

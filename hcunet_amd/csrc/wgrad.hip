@@ -625,12 +625,13 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   long kb = std::max(1L, (long)target_blocks / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
-  if (!wgrad2_disabled()) plan_wgrad2(a, target_blocks);
+  if (plan_wgrad8(a) != 0 && !wgrad2_disabled()) plan_wgrad2(a, target_blocks);
   return 0;
 }
 
 int launch_wgrad(const WGradArgs &a, hipStream_t s) {
   if (a.use_bw) return launch_bwgrad(a, s);
+  if (a.v2 == 2) return launch_wgrad8(a, s);
   const dim3 grid(a.KB, a.mchunks, a.nchunks);
   const int T = a.KX * a.KY * a.KZ;
   if (a.v2) {

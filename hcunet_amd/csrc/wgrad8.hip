@@ -1,0 +1,569 @@
+// Weight gradient of a stride-1 Conv3d with few output channels, with no
+// padded MFMA columns (hcat/unet.py:246-257 on the 8- and 16-channel levels:
+// Conv3d k=(3,3,2) / (3,3,1), 4->8, 8->8, 8->16, 16->16 at up to 254x254x15).
+//
+//   dW[(kx,ky,kz,ci)][co] = sum_p act(A)[px+kx, py+ky, pz+kz*dz][ci] * G[p][co]
+//
+// With 8 output channels the 16 columns of v_mfma_f32_16x16x4f32 are half
+// padding.  Two moves remove it:
+//  * the z tap goes to the column side: with q = pz + kz*dz,
+//      dW[(kx,ky,ci)][(kz,co)] = sum_q act(A)[px+kx, py+ky, q][ci] * G[px, py, q - kz*dz][co]
+//    (G = 0 outside its extent), so a row's A operand no longer depends on kz;
+//  * form 1 runs v_mfma_f32_4x4x1_16b_f32 (16 independent 4x4 blocks, the same
+//    FLOP rate): block b = (voxel set v, z tap j, channel quad cq), rows = 4
+//    input channels of one (kx, ky) tap, so an instruction is 16/(KZ*GCs/4)
+//    voxels x 4 rows x KZ*GCs columns, all real; the voxel sets are summed at
+//    the end.  Form 0 keeps 16x16x4 for KZ*GCs = 16 (rows (kx,ky,ci) + bias).
+//
+// LDS images: A halo [ci][hx][hy][q] (no z halo: the 16-long q run IS the A
+// z range), G [co][x][y][slot] with slot = 4 + z, so z = -1 is slot 3.  A lane
+// reads 4 z-consecutive voxels with ONE ds_read_b128; a column shifted by one
+// z takes (slot 3+4g, slots 4+4g..6+4g) through one extra ds_read_b32 and three
+// selects.  The next tile's A and G are loaded into registers while the
+// current one computes (BatchNorm+ReLU of the producer applied when they are
+// stored, from an LDS copy of the coefficients), then transposed in registers
+// to b128 stores.  Two workgroups per CU, persistent over contiguous tile
+// ranges; each writes one fp32 partial slab (wgrad_finalize sums them in a
+// fixed order).
+#include "common.h"
+#include "timing.h"
+#include <algorithm>
+#include <cstdlib>
+
+namespace hcu {
+
+// MODE 0: NR = row tiles of 16 (rows (kx,ky,ci) + bias).  MODE 1: NR = row
+// quads per wave; the plan's a.MS quads ((kx,ky,ci quad) + the bias quad last)
+// are split over a.w8nh wave groups, each taking every (4/w8nh)-th K-step.
+template <int MODE, int NR>
+__global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ __attribute__((aligned(16))) char sa_raw[sizeof(WGradArgs)];
+  __shared__ __attribute__((aligned(16))) float actl[2][32];  // BN scale / shift of this chunk
+  WGradArgs &sa = *reinterpret_cast<WGradArgs *>(sa_raw);
+#define KA(f) kuni(sa.f)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: scalar loop control
+  {  // cooperative copy of the arguments (the offset table is read per lane below)
+    const int *src = reinterpret_cast<const int *>(&a);
+    int *dst = reinterpret_cast<int *>(sa_raw);
+    for (int i = tid; i < (int)(sizeof(WGradArgs) / 4); i += 256) dst[i] = src[i];
+  }
+  const int CKA = a.CKA, CA4 = CKA >> 2, GCs = a.GCs, CG4 = GCs >> 2;
+  const int cic = blockIdx.y, ci0 = cic * CKA;
+  const int HY = a.HAY, ARS = a.ARS, APL = a.PA2, GPL = a.PG2;
+  constexpr int GRS = 20;
+  float *alds = smem;                                // [CKA][HX*HY][ARS] (+ MODE 1: a plane of ones)
+  float *glds = smem + (size_t)(CKA + MODE) * APL;   // [GCs][TX*TY][GRS]
+  const int KXY = a.KX * a.KY;
+  const bool bias_block = a.bias_row && cic == 0;
+  const bool act = a.a_scale != nullptr;
+
+  for (int i = tid; i < (CKA + MODE) * APL + GCs * GPL; i += 256)
+    smem[i] = (MODE == 1 && i >= CKA * APL && i < (CKA + 1) * APL) ? 1.f : 0.f;
+  if (tid < CKA) {
+    actl[0][tid] = act ? a.a_scale[ci0 + tid] : 1.f;
+    actl[1][tid] = act ? a.a_shift[ci0 + tid] : 0.f;
+  }
+
+  lds_barrier();
+  if (a.w8dbg & 8) return;
+  // ---- lane roles
+  constexpr int NACC = NR;
+  int aoff[NR];
+  int abase = 0, gbase = 0, vc = 0, q0 = 0, nh = 1;
+  bool sh = false;
+  float amul = 1.f, aadd = 0.f;
+  const int NQ = a.MS, NP = NQ - 1;                  // MODE 1: quads in all, plain quads
+  int nrow = KXY * CKA;
+  if constexpr (MODE == 0) {
+    const int g = lane >> 4, r16 = lane & 15;
+#pragma unroll
+    for (int ms = 0; ms < NR; ++ms) aoff[ms] = sa.w8off[ms * 16 + r16];   // plan_wgrad8 table
+    const int rl = (NR - 1) * 16 + r16;              // the last row tile holds every non-plain row
+    amul = rl < nrow ? 1.f : 0.f;
+    aadd = (bias_block && rl == nrow) ? 1.f : 0.f;
+    const int kzc = r16 / GCs, coc = r16 - kzc * GCs;
+    sh = kzc * a.adz != 0;                           // this column reads G[q - 1]
+    abase = 4 * g;
+    gbase = coc * GPL + 4 * g;
+  } else {
+    const int bq = lane >> 2, ii = lane & 3;
+    const int NBv = a.w8nbv, NJ = a.w8nj;
+    const int v = bq % NBv, jc = bq / NBv, j = jc % NJ, cq = jc / NJ;
+    vc = v >> 2;
+    const int vz = v & 3;
+    nh = a.w8nh;
+    q0 = (wave % nh) * NR;
+    // quads past the last are computed on plane 0 and never written; the bias
+    // quad reads the ones plane (only its row 0, lane ii = 0, is written)
+#pragma unroll
+    for (int k = 0; k < NR; ++k)                     // per lane: VGPRs
+      aoff[k] = q0 + k == NP ? CKA * APL + 4 * vz : ii * APL + 4 * vz + sa.w8off[q0 + k];
+    gbase = (4 * cq + ii) * GPL + 4 * vz;
+    sh = j * a.adz != 0;
+  }
+
+  floatx4 acc[NACC];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int NXY = a.TX * a.TY;
+  const int nA = CA4 * a.HAX * HY * 4;
+  const int nzq = a.ntz > 1 ? 5 : 4;                 // z quad -1 (slot 3) only when z tiles have a predecessor
+  const int nG = CG4 * NXY * nzq;
+  const FastDiv fTY = a.fTY;
+  const int tpb = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_beg = (int)blockIdx.x * tpb;
+  const int t_end = min(total, t_beg + tpb);
+
+  // staging cells of this thread (at most 2 A and 2 G cells: plan_wgrad8)
+  int adst[2], gdst[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int ia = tid + u * 256;
+    adst[u] = -1;
+    if (ia < nA) {
+      const int cq = ia % CA4, rest = ia / CA4, zq = rest & 3, hxy = rest >> 2;
+      adst[u] = (cq * 4) * APL + hxy * ARS + zq * 4;
+    }
+    const int ig = tid + u * 256;
+    gdst[u] = -1;
+    if (ig < nG) {
+      const int cq = ig % CG4, rest = ig / CG4, zr = rest % nzq, xy = rest / nzq;
+      gdst[u] = (cq * 4) * GPL + xy * GRS + 4 + (zr - (nzq - 4)) * 4;
+    }
+  }
+  floatx4 ra[2][4], rg[2][4];
+  int ma = 0;                                        // valid A voxels: bit u*4 + j
+
+  const int dbg = a.w8dbg;   // HCU_W8_DBG (measurement only): 1 no MFMA, 2 no loads, 4 no LDS stores
+  // Branch-free buffer loads straight into the prefetch registers (a load under
+  // a branch is copied at the join, which waits for it): invalid positions read
+  // an offset past the sample's buffer and return 0.
+  constexpr int OOB = 0x7ffffff0;
+  auto load = [&](int tt) {
+    if (dbg & 2) return;
+    const int b = tt / ntiles;
+    int tile = tt - b * ntiles;
+    const int tyi = tile % KA(nty);
+    tile /= KA(nty);
+    const int txi = tile % KA(ntx), tzi = tile / KA(ntx);
+    const int x0 = txi * KA(TX), y0 = tyi * KA(TY), z0 = tzi * 16;
+    ma = 0;
+    const int AX = KA(AX), AY = KA(AY), AZ = KA(AZ), ACs = KA(ACs);
+    const size_t sampA = (size_t)AX * AY * AZ * ACs;
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(KA(A) + b * sampA), 0, (int)(sampA * 4), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ia = tid + u * 256;
+      const int cq = ia % CA4, rest = ia / CA4, zq = rest & 3, hxy = rest >> 2;
+      int hx, hy;
+      sa.fHAY.uni().divmod(hxy, hx, hy);
+      const int x = x0 + hx, y = y0 + hy, zb = z0 + zq * 4;
+      const bool okc = ia < nA && x < AX && y < AY;
+      const int base = (((x * AY + y) * AZ + zb) * ACs + ci0 + cq * 4) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = okc && zb + j < AZ;
+        ra[u][j] = __builtin_bit_cast(floatx4,
+                                      __builtin_amdgcn_raw_buffer_load_b128(rsA, ok ? base + j * ACs * 4 : OOB, 0, 0));
+        ma |= (ok ? 1 : 0) << (u * 4 + j);
+      }
+    }
+    const int PX = KA(PX), PY = KA(PY), PZ = KA(PZ), GX = KA(GX), GY = KA(GY), GZ = KA(GZ);
+    const size_t sampG = (size_t)GX * GY * GZ * GCs;
+    const __amdgpu_buffer_rsrc_t rsG =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(KA(G) + b * sampG), 0, (int)(sampG * 4), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ig = tid + u * 256;
+      const int cq = ig % CG4, rest = ig / CG4, zr = rest % nzq, xy = rest / nzq;
+      int lx, ly;
+      sa.fTY.uni().divmod(xy, lx, ly);
+      const int x = x0 + lx, y = y0 + ly, zb = z0 + (zr - (nzq - 4)) * 4;
+      const bool okc = ig < nG && x < PX && y < PY;
+      const int base = (((x * GY + y) * GZ + zb) * GCs + cq * 4) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int z = zb + j;
+        const bool ok = okc && z >= 0 && z < PZ;
+        rg[u][j] = __builtin_bit_cast(floatx4,
+                                      __builtin_amdgcn_raw_buffer_load_b128(rsG, ok ? base + j * GCs * 4 : OOB, 0, 0));
+      }
+    }
+  };
+
+  lds_barrier();
+  if (dbg & 32) return;
+  if (t_beg < t_end) load(t_beg);
+  for (int tt = t_beg; tt < t_end; ++tt) {
+    lds_barrier();
+    // ---- registers -> LDS (activation on A), transposed to z-major b128 stores
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (adst[u] < 0 || (dbg & 4)) continue;
+      const int cq = (tid + u * 256) % CA4;
+      const floatx4 sc = *reinterpret_cast<const floatx4 *>(&actl[0][cq * 4]);
+      const floatx4 sf = *reinterpret_cast<const floatx4 *>(&actl[1][cq * 4]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = (ma >> (u * 4 + j)) & 1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = act ? fmaxf(fmaf(ra[u][j][e], sc[e], sf[e]), 0.f) : ra[u][j][e];
+          ra[u][j][e] = ok ? t : 0.f;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        *reinterpret_cast<floatx4 *>(alds + adst[u] + c * APL) =
+            floatx4{ra[u][0][c], ra[u][1][c], ra[u][2][c], ra[u][3][c]};
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (gdst[u] < 0 || (dbg & 4)) continue;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        *reinterpret_cast<floatx4 *>(glds + gdst[u] + c * GPL) =
+            floatx4{rg[u][0][c], rg[u][1][c], rg[u][2][c], rg[u][3][c]};
+    }
+    lds_barrier();
+    if (tt + 1 < t_end) load(tt + 1);                // lands while this tile computes
+    if (dbg & 1) continue;
+    // K-steps of this wave (form 0: one tile column each, wave w takes w, w+4, ..;
+    // form 1: NBv/4 columns each, wave w takes w/nh, w/nh + 4/nh, ..), software
+    // pipelined: the next step's LDS reads are issued before this step's MFMAs
+    // (a step past the end re-reads the last one; its operands are unused).
+    const int ncol = MODE == 0 ? 1 : (a.w8nbv >> 2);
+    const int nks = NXY / ncol;
+    const int ks0 = MODE == 0 ? wave : wave / nh;
+    const int kst = MODE == 0 ? 4 : 4 / nh;
+    if (ks0 < nks) {
+      auto rd = [&](int ks, floatx4 (&av)[NR], floatx4 &bq, float &bp) {
+        const int col = ks * ncol + vc;
+        int lx, ly;
+        fTY.divmod(col, lx, ly);
+        const int ox = (lx * HY + ly) * ARS + abase;
+        const int gxy = gbase + col * GRS + 4;
+        bq = *reinterpret_cast<const floatx4 *>(glds + gxy);
+        bp = glds[gxy - 1];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) av[k] = *reinterpret_cast<const floatx4 *>(alds + aoff[k] + ox);
+      };
+      auto mm = [&](floatx4 (&av)[NR], const floatx4 &bq, float bp) {
+        floatx4 bv;
+        bv[0] = sh ? bp : bq[0];
+        bv[1] = sh ? bq[0] : bq[1];
+        bv[2] = sh ? bq[1] : bq[2];
+        bv[3] = sh ? bq[2] : bq[3];
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) av[NR - 1][e] = fmaf(av[NR - 1][e], amul, aadd);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int ms = 0; ms < NR; ++ms)
+              acc[ms] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ms][c], bv[c], acc[ms], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int k = 0; k < NR; ++k)   // NR independent accumulators between dependent MFMAs
+              acc[k] = __builtin_amdgcn_mfma_f32_4x4x1f32(av[k][c], bv[c], acc[k], 0, 0, 0);
+        }
+      };
+      floatx4 a0[NR], a1[NR], b0, b1;
+      float p0, p1;
+      rd(ks0, a0, b0, p0);
+      // sched_barrier pins the order (the scheduler would sink the reads to their use)
+      for (int ks = ks0;;) {
+        rd(min(ks + kst, nks - 1), a1, b1, p1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(a0, b0, p0);
+        __builtin_amdgcn_sched_barrier(0);
+        ks += kst;
+        if (ks >= nks) break;
+        rd(min(ks + kst, nks - 1), a0, b0, p0);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(a1, b1, p1);
+        __builtin_amdgcn_sched_barrier(0);
+        ks += kst;
+        if (ks >= nks) break;
+      }
+    }
+  }
+
+  if (dbg & 16) return;
+  // ---- every wave stores its accumulators (b128, no serial rounds), then the
+  // fixed-order sum over waves (and, form 1, over the voxel blocks)
+  lds_barrier();
+  float *red = smem;  // [wave][NR][64 lanes][4]
+#pragma unroll
+  for (int i = 0; i < NACC; ++i)
+    *reinterpret_cast<floatx4 *>(red + ((wave * NR + i) * 64 + lane) * 4) = acc[i];
+  lds_barrier();
+  const int kb = blockIdx.x;
+  const int T = KXY * a.KZ;
+  if constexpr (MODE == 0) {
+    for (int idx = tid; idx < NR * 256; idx += 256) {
+      const int r = idx & 3, ln = (idx >> 2) & 63, ms = idx >> 8;
+      const float s = ((red[idx] + red[NR * 256 + idx]) + red[2 * NR * 256 + idx]) + red[3 * NR * 256 + idx];
+      const int lr = ms * 16 + (ln >> 4) * 4 + r;
+      const int lc = ln & 15, kz = lc / GCs, co = lc - kz * GCs;
+      int grow = -1;
+      if (lr < nrow) {
+        const int kxy = lr / CKA, c = lr - kxy * CKA;
+        grow = (kxy * a.KZ + kz) * a.ACs + ci0 + c;   // tap t = (kx*KY + ky)*KZ + kz
+      } else if (bias_block && lr == nrow && kz == 0) {
+        grow = T * a.ACs;
+      }
+      if (grow >= 0) a.partial[((size_t)kb * a.Mtot + grow) * a.Ntot + co] = s;
+    }
+  } else {
+    // element (row quad q, row r, column group jc = cq*NJ + j, column i)
+    const int NBv = a.w8nbv, NJ = a.w8nj, EPR = 256 / NBv, np = 4 / nh;
+    for (int idx = tid; idx < NQ * EPR; idx += 256) {
+      const int q = idx / EPR, rem = idx - q * EPR;
+      const int r = rem & 3, i = (rem >> 2) & 3, jc = rem >> 4;
+      const int h = q / NR, k = q - h * NR;
+      float s = 0.f;
+      for (int p = 0; p < np; ++p) {
+        const float *src = red + (((h + p * nh) * NR + k) * 64 + jc * NBv * 4 + i) * 4 + r;
+        for (int v = 0; v < NBv; ++v) s += src[v * 16];
+      }
+      const int j = jc % NJ, cq = jc / NJ;
+      int grow = -1;
+      if (q < NP) {
+        const int kxy = q / CA4, ciq = q - kxy * CA4;
+        grow = (kxy * a.KZ + j) * a.ACs + ci0 + ciq * 4 + r;
+      } else if (bias_block && r == 0 && j == 0) {
+        grow = T * a.ACs;
+      }
+      if (grow >= 0) a.partial[((size_t)kb * a.Mtot + grow) * a.Ntot + cq * 4 + i] = s;
+    }
+  }
+#undef KA
+}
+
+// Worst b128 bank conflict (distinct 16-byte addresses per slot within one
+// LDS cycle) of one wave's reads, over the four lane groups of ds_read_b128
+// (MI355X_MICROARCH.md, LDS table).
+static int b128_conflict(const int *dw /*[64] dword addresses*/) {
+  static const int grp[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  int worst = 1;
+  for (int q = 0; q < 4; ++q) {
+    int n[16] = {0}, seen[16];
+    int ns = 0;
+    for (int i = 0; i < 16; ++i) {
+      const int d = dw[grp[q][i]];
+      bool dup = false;
+      for (int j = 0; j < ns; ++j) dup |= seen[j] == d;
+      if (dup) continue;
+      seen[ns++] = d;
+      worst = std::max(worst, ++n[(d >> 2) & 15]);
+    }
+  }
+  return worst;
+}
+
+// dynamic LDS per workgroup: two workgroups (plus their static LDS) per CU
+static constexpr long kW8LdsFloats = 76 * 1024 / 4;   // + ~1.3 KB static
+
+static bool w8_nr_supported(int mode, int nr) {
+  if (mode == 0) return nr >= 1 && nr <= 8;
+  return nr >= 2 && nr <= 40;   // split over up to 4 wave groups of <= 10 quads
+}
+
+// Re-plans a Conv3d weight gradient for wgrad8_kernel; returns 0 when it applies.
+int plan_wgrad8(WGradArgs &a) {
+  if (getenv("HCU_NO_WGRAD8") && getenv("HCU_NO_WGRAD8")[0] == '1') return 1;
+  if (!a.taps_rows || a.asx != 1 || a.asy != 1 || a.asz != 1 || a.gsx != 1 || a.gsy != 1 ||
+      a.gsz != 1 || a.apx || a.apy || a.apz || a.gpx || a.gpy || a.gpz)
+    return 1;
+  if (a.ACs % 4 || a.GCs % 4 || (a.KZ - 1) * a.adz > 1) return 1;
+  if (a.AZ != a.PZ + (a.KZ - 1) * a.adz || a.AX < a.PX + (a.KX - 1) * a.adx ||
+      a.AY < a.PY + (a.KY - 1) * a.ady || a.GX < a.PX || a.GY < a.PY || a.GZ < a.PZ)
+    return 1;
+  if ((double)a.AX * a.AY * a.AZ * a.ACs * 4 >= 2147483000.0 ||
+      (double)a.GX * a.GY * a.GZ * a.GCs * 4 >= 2147483000.0)
+    return 1;   // per-sample buffer resources address at most 2^31 bytes
+  // form 0 (16x16x4) where the z taps fill the 16 columns: per MFMA cycle it
+  // issues a quarter of form 1's operand reads and address arithmetic
+  // (measured on the 4->8 level-0 conv: 50 us vs 57 us); form 1 otherwise
+  int mode;
+  if (a.GCs * a.KZ == 16) mode = 0;
+  else if (a.GCs <= 8 && a.KZ <= 2 && a.KZ * a.GCs <= 16) mode = 1;
+  else return 1;
+  if (getenv("HCU_WGRAD8_MODE")) {   // A/B testing: force a form where it applies
+    const int m = atoi(getenv("HCU_WGRAD8_MODE"));
+    if (m == 1 && a.GCs <= 8 && a.KZ <= 2) mode = 1;
+  }
+  const int KXY = a.KX * a.KY;
+  const int NJ = a.KZ, NBv = mode == 1 ? 16 / (NJ * (a.GCs / 4)) : 0, NCOL = mode == 1 ? NBv / 4 : 1;
+  int nci = 0, NR = 0;
+  for (int n = 1; n <= a.ACs / 4; ++n) {
+    if (a.ACs % (4 * n) || a.ACs / n > 32) continue;
+    const int cka = a.ACs / n;
+    const int nr = mode == 0 ? cdiv(KXY * cka + 1, 16) : KXY * cka / 4 + 1;
+    if (w8_nr_supported(mode, nr)) {
+      nci = n;
+      NR = nr;
+      break;
+    }
+  }
+  if (!nci) return 1;
+  const int CKA = a.ACs / nci, CA4 = CKA / 4, CG4 = a.GCs / 4;
+  const int ntz = cdiv(a.PZ + (a.KZ - 1) * a.adz, 16);
+  const int nzq = ntz > 1 ? 5 : 4;
+  const int tiles[4][2] = {{8, 8}, {8, 4}, {4, 8}, {4, 4}};
+  bool found = false;
+  for (int i = 0; i < 4 && !found; ++i) {
+    const int TX = std::min(tiles[i][0], a.PX), TY = std::min(tiles[i][1], a.PY);
+    const int HX = TX + (a.KX - 1) * a.adx, HY = TY + (a.KY - 1) * a.ady;
+    if ((TX * TY) % NCOL) continue;
+    if (CA4 * HX * HY * 4 > 512 || CG4 * TX * TY * nzq > 512) continue;
+    // G planes: GPL = 8 (mod 64) floats spreads (channel, z quad) over the 16 slots
+    const int gbase = TX * TY * 20;
+    const int GPL = gbase + ((8 - gbase % 64) % 64 + 64) % 64;
+    // bank-conflict-aware strides: A z rows of 16 or 20 floats, plane pads
+    int best_c = 1 << 30, ARS = 16, APL = 0;
+    for (int rs : {16, 20}) {
+      const int base = HX * HY * rs;
+      for (int pad = 0; pad < 64; pad += 4) {
+        const int pl = round_up(base, 4) + pad;
+        auto tapoff = [&](int kxy) {
+          const int kx = kxy / a.KY, ky = kxy % a.KY;
+          return (kx * a.adx * HY + ky * a.ady) * rs;
+        };
+        auto colA = [&](int xy) { return ((xy / TY) * HY + xy % TY) * rs; };
+        int worst = 1;
+        const int nsteps = std::min(2, TX * TY / NCOL);
+        if (mode == 0) {
+          for (int ms = 0; ms < NR; ++ms)
+            for (int ks = 0; ks < nsteps; ++ks) {
+              int dw[64];
+              for (int l = 0; l < 64; ++l) {
+                const int r = ms * 16 + (l & 15);
+                int off = 0;
+                if (r < KXY * CKA) off = (r % CKA) * pl + tapoff(r / CKA);
+                dw[l] = off + colA(ks) + 4 * (l >> 4);
+              }
+              worst = std::max(worst, b128_conflict(dw));
+            }
+        } else {
+          for (int rq = 0; rq < NR - 1; ++rq)
+            for (int ks = 0; ks < nsteps; ++ks) {
+              int dw[64];
+              for (int l = 0; l < 64; ++l) {
+                const int v = (l >> 2) % NBv, ii = l & 3;
+                dw[l] = ii * pl + (rq % CA4) * 4 * pl + tapoff(rq / CA4) + colA(ks * NCOL + (v >> 2)) +
+                        4 * (v & 3);
+              }
+              worst = std::max(worst, b128_conflict(dw));
+            }
+        }
+        const int cost = worst * 1024 + pad + (rs - 16);
+        if ((long)(CKA + mode) * pl + (long)a.GCs * GPL > kW8LdsFloats) continue;
+        if (cost < best_c) {
+          best_c = cost;
+          ARS = rs;
+          APL = pl;
+        }
+      }
+    }
+    if (!APL) continue;
+    const int nrw = mode == 0 ? NR : cdiv(NR, NR > 10 ? (NR > 20 ? 4 : 2) : 1);   // accumulators per wave
+    const long lds = std::max((long)(CKA + mode) * APL + (long)a.GCs * GPL, 4L * nrw * 256) * 4;
+    if (lds > kW8LdsFloats * 4) continue;
+    a.TX = TX;
+    a.TY = TY;
+    a.HAX = HX;
+    a.HAY = HY;
+    a.ARS = ARS;
+    a.PA2 = APL;
+    a.PG2 = GPL;
+    a.lds_bytes = (int)lds;
+    found = true;
+  }
+  if (!found) return 1;
+  a.CKA = CKA;
+  a.nci = nci;
+  a.MS = NR;
+  a.w8nh = 1;
+  if (mode == 1)
+    while (cdiv(NR, a.w8nh) > 10) a.w8nh *= 2;
+  {  // A image offsets per row (form 0) / per row quad (form 1), without the lane part
+    const int nslots = mode == 0 ? NR * 16 : a.w8nh * cdiv(NR, a.w8nh);
+    if (nslots > 128) return 1;
+    for (int r = 0; r < 128; ++r) a.w8off[r] = 0;
+    for (int r = 0; r < nslots; ++r) {
+      const int per = mode == 0 ? CKA : CA4;          // rows (channels) / quads per tap
+      if (r >= KXY * per) continue;
+      const int kxy = r / per, c = r % per, kx = kxy / a.KY, ky = kxy % a.KY;
+      a.w8off[r] = (mode == 0 ? c : 4 * c) * a.PA2 + (kx * a.adx * a.HAY + ky * a.ady) * a.ARS;
+    }
+  }
+  a.NS = 1;
+  a.w8mode = mode;
+  a.w8nbv = NBv;
+  a.w8nj = NJ;
+  a.ntx = cdiv(a.PX, a.TX);
+  a.nty = cdiv(a.PY, a.TY);
+  a.ntz = ntz;
+  a.fHAY = FastDiv(a.HAY);
+  a.fTY = FastDiv(a.TY);
+  // two workgroups per CU; among grid sizes that keep them, the one with the
+  // least MFMA work at the slowest CU (tiles are equal-cost)
+  const long total = (long)a.B * a.ntx * a.nty * a.ntz;
+  long best_kb = 1, best_cost = 1L << 62;
+  for (int per_cu = 1; per_cu <= 2; ++per_cu) {
+    const long kb = std::min(total, (long)256 * per_cu / nci);
+    if (kb < 1) continue;
+    const long cost = cdiv(total, kb) * per_cu;
+    if (cost < best_cost || (cost == best_cost && kb > best_kb)) {
+      best_cost = cost;
+      best_kb = kb;
+    }
+  }
+  a.KB = (int)std::max(1L, best_kb);
+  a.w8dbg = getenv("HCU_W8_DBG") ? atoi(getenv("HCU_W8_DBG")) : 0;
+  a.v2 = 2;
+  return 0;
+}
+
+int launch_wgrad8(const WGradArgs &a, hipStream_t s) {
+  const dim3 grid(a.KB, a.nci, 1);
+  const int T = a.KX * a.KY * a.KZ;
+  const double fl = a.flops > 0 ? a.flops : 2.0 * a.B * a.PX * a.PY * a.PZ * (double)T * a.ACs * a.GCs;
+  const double by = 4.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
+                           (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
+  bool ok = false;
+#define W8(MODE_, NR_)                                                                              \
+  if (!ok && a.w8mode == MODE_ && a.MS == NR_) {                                                    \
+    HCU_TIMED(s, "wgrad8_kernel<" #MODE_ "," #NR_ ">", fl, by,                                      \
+              hipLaunchKernelGGL((wgrad8_kernel<MODE_, NR_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    ok = true;                                                                                      \
+  }
+  W8(0, 1) W8(0, 2) W8(0, 3) W8(0, 4) W8(0, 5) W8(0, 6) W8(0, 7) W8(0, 8)
+#undef W8
+#define W8Q(NRW_)                                                                             \
+  if (!ok && a.w8mode == 1 && cdiv(a.MS, a.w8nh) == NRW_) {                                   \
+    HCU_TIMED(s, "wgrad8_kernel<1," #NRW_ ">", fl, by,                                        \
+              hipLaunchKernelGGL((wgrad8_kernel<1, NRW_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    ok = true;                                                                                \
+  }
+  W8Q(2) W8Q(3) W8Q(4) W8Q(5) W8Q(6) W8Q(7) W8Q(8) W8Q(9) W8Q(10)
+#undef W8Q
+  if (!ok) return fail(4, "wgrad8: unsupported row tiling");
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu

@@ -25,6 +25,12 @@ CONV_CASES = [
     (2, 6, 12, 9, 10, 6, (3, 3, 3), (1, 1, 1), 1),
     (1, 3, 5, 9, 9, 4, (1, 1, 1), (1, 1, 1), 1),
     (1, 4, 8, 10, 10, 20, (3, 3, 2), (1, 1, 1), 1),
+    # wgrad8 (z tap on the column side): 8->8 at the level-0 depth, 16 columns
+    # with KZ=1, two row chunks (16 input channels), ragged x/y tiles
+    (1, 8, 8, 19, 21, 16, (3, 3, 2), (1, 1, 1), 1),
+    (2, 8, 16, 13, 12, 9, (3, 3, 1), (1, 1, 1), 1),
+    (1, 16, 8, 12, 11, 10, (3, 3, 2), (1, 1, 1), 1),
+    (1, 8, 8, 11, 9, 35, (3, 3, 2), (1, 1, 1), 1),
 ]
 
 
