@@ -96,6 +96,15 @@ SYMBOLS = [
     ("hcu_loss_pixel_fwd", _I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _I, _I, _I,
                                 _VP, _VP, _VP, _SZ, _VP]),
     ("hcu_scale_by_device_scalar", _I, [_VP, _VP, _VP, _I64, _VP]),
+    ("hcu_loss_ext_scratch_bytes", _SZ, [_I, _I64, _I]),
+    ("hcu_loss_ext_fwd", _I, [_I, _VP, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP,
+                              _VP, _SZ, _VP]),
+    ("hcu_loss_ext_bwd", _I, [_I, _VP, _I, _I, _I, _I, _I, _VP, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP,
+                              _VP, _VP]),
+    ("hcu_loss_random_rows", _I, [_I64]),
+    ("hcu_loss_random_count", _I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _I, _VP, _VP]),
+    ("hcu_loss_random_fwd", _I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP,
+                                 _I, _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("hcu_adam_step", _I, [_VP, _VP, _VP, _VP, _I64, _F, _F, _F, _F, _F, _I64, _F, _VP]),
     ("hcu_conv_scratch_bytes", _SZ, [ctypes.POINTER(ConvDesc)]),
     ("hcu_conv_out_dims", _I, [ctypes.POINTER(ConvDesc), ctypes.POINTER(_I)]),

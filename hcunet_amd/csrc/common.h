@@ -452,12 +452,15 @@ inline size_t wprep_floats(const GConvArgs &a) {
   const WPack p = wpack_of(a);
   return (size_t)a.ICs * p.S * (16 / p.CK) * a.CoutW;
 }
-// Packed index -> (t, ci, co); false for a padded tap.
-__device__ __forceinline__ bool wpack_decode(const WPack &p, int64_t i, int T, int &t, int &ci,
+// Packed index -> (t, ci, co); false for a padded tap.  I = uint32_t where the
+// caller knows the image has < 2^31 elements (64-bit division is a ~100
+// instruction software sequence).
+template <typename I>
+__device__ __forceinline__ bool wpack_decode(const WPack &p, I i, int T, int &t, int &ci,
                                              int &co) {
   if (p.on == 3) {
     const int j = (int)(i & 7);
-    int64_t q = i >> 3;
+    I q = i >> 3;
     co = (int)(q % p.CoutW);
     q /= p.CoutW;
     const int g = (int)(q & 3);
@@ -478,7 +481,7 @@ __device__ __forceinline__ bool wpack_decode(const WPack &p, int64_t i, int T, i
     return t < T;
   }
   const int j = (int)(i & 3);
-  int64_t q = i >> 2;
+  I q = i >> 2;
   co = (int)(q % p.CoutW);
   q /= p.CoutW;
   const int g = (int)(q & 3);

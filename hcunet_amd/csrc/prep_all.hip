@@ -15,13 +15,13 @@ struct PrepBatch {
   PrepJob j[kPrepBatch];
 };
 
-__device__ __forceinline__ bool prep_index2(const WPack &pk, int64_t i, int T, int ICs, int CoutW,
+__device__ __forceinline__ bool prep_index2(const WPack &pk, uint32_t i, int T, int ICs, int CoutW,
                                             int &t, int &ci, int &co) {
   if (pk.on) return wpack_decode(pk, i, T, t, ci, co);
-  co = (int)(i % CoutW);
-  const int64_t q = i / CoutW;
-  ci = (int)(q % ICs);
-  t = (int)(q / ICs);
+  co = (int)(i % (uint32_t)CoutW);
+  const uint32_t q = i / (uint32_t)CoutW;
+  ci = (int)(q % (uint32_t)ICs);
+  t = (int)(q / (uint32_t)ICs);
   return true;
 }
 
@@ -38,7 +38,7 @@ __device__ __forceinline__ float weff2(const float *w, int o, int e, int t, int 
   return s;
 }
 
-__device__ float prep_value(const PrepJob &jb, const float *w, int64_t i) {
+__device__ float prep_value(const PrepJob &jb, const float *w, uint32_t i) {
   const int *p = jb.p;
   switch (jb.kind) {
     case PREP_CONV_FWD: {
@@ -72,10 +72,10 @@ __device__ float prep_value(const PrepJob &jb, const float *w, int64_t i) {
     case PREP_CONVT_PHASE: {
       const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
       const int Jx = p[11], Jy = p[12], Jz = p[13], ICs = p[14], CoutW = p[15];
-      const int co = (int)(i % CoutW);
-      const int64_t q = i / CoutW;
-      const int ci = (int)(q % ICs);
-      const int t = (int)(q / ICs);
+      const int co = (int)(i % (uint32_t)CoutW);
+      const uint32_t q = i / (uint32_t)CoutW;
+      const int ci = (int)(q % (uint32_t)ICs);
+      const int t = (int)(q / (uint32_t)ICs);
       const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
       const int kx = p[8] + p[5] * (Jx - 1 - tx), ky = p[9] + p[6] * (Jy - 1 - ty),
                 kz = p[10] + p[7] * (Jz - 1 - tz);
@@ -97,15 +97,14 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
   const PrepJob &jb = b.j[blockIdx.y];
   const float *w = params + jb.src;
   float *dst = dst_base + jb.dst;
+  const uint32_t n = (uint32_t)jb.n;   // < 2^31 (launch_prep_all)
   if (jb.bf16) {
     uint16_t *d16 = reinterpret_cast<uint16_t *>(dst);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < jb.n;
-         i += (int64_t)gridDim.x * 256)
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
       d16[i] = f2bf(prep_value(jb, w, i));
     return;
   }
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < jb.n;
-       i += (int64_t)gridDim.x * 256)
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
     dst[i] = prep_value(jb, w, i);
 }
 
@@ -118,8 +117,10 @@ int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, i
     for (int k = 0; k < b.n; ++k) {
       b.j[k] = jobs[j0 + k];
       most = std::max(most, b.j[k].n);
+      if (b.j[k].n >= (int64_t)1 << 31) return fail(4, "prep_all: weight image too large");
     }
-    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((most + 255) / 256, 128));
+    // enough workgroups that the largest job is ~8 elements per thread
+    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((most + 2047) / 2048, 1024));
     HCU_TIMED(s, "prep_all_kernel", 0.0, 0.0,
               hipLaunchKernelGGL(prep_all_kernel, dim3(gx, b.n), dim3(256), 0, s, params,
                                  dst_base, b));

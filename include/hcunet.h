@@ -181,6 +181,44 @@ int hcu_scale_by_device_scalar(const float *src, const float *scale, float *dst,
                                int64_t n, hcu_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* The reference's other losses (hcat/loss.py:5-178), same geometry as     */
+/* hcu_loss_pixel_fwd.  mode: 0 cross_entropy(method='sigmoid') (:38-40,     */
+/* :95-97), 1 method='worst_z' (:74-80), 2 dice (:104-126), 3 L1Loss         */
+/* (:128-152), 4 MSELoss (:154-178), 5 plain BCE mean ('random' with no      */
+/* positive pixel, :84-85), 6 'random' (hcu_loss_random_fwd, :86-93).        */
+/* Forward writes loss[0] and aux (the scalars the gradient needs: 1 float,  */
+/* 2 for dice, PZ for worst_z); backward writes dpred = dloss/dpred *        */
+/* grad_out[0].  zscale (worst_z): torch.linspace(1, 2, PZ) ** 2 (:76).      */
+/* ------------------------------------------------------------------------ */
+size_t hcu_loss_ext_scratch_bytes(int mode, int64_t n_pred, int PZ);
+int hcu_loss_ext_fwd(int mode, const float *pred, int B, int C, int PX, int PY, int PZ,
+                     const void *mask, int mask_dtype, const void *pwl, int pwl_dtype,
+                     int MX, int MY, int MZ, const float *zscale, float *loss, float *aux,
+                     void *scratch, size_t scratch_bytes, hcu_stream_t stream);
+int hcu_loss_ext_bwd(int mode, const float *pred, int B, int C, int PX, int PY, int PZ,
+                     const void *mask, int mask_dtype, const void *pwl, int pwl_dtype,
+                     int MX, int MY, int MZ, const float *aux, const int *counts,
+                     const float *grad_out, float *dpred, hcu_stream_t stream);
+/* 'random' (hcat/loss.py:82-93): rows = hcu_loss_random_rows(n);
+ * hcu_loss_random_count writes counts[rows][2] = (#mask==1, #mask==0) per row
+ * of the flattened cropped mask; the caller draws pos_ind / neg_ind (int64,
+ * n each) from its generator as the reference does and passes the exclusive
+ * row offsets; hcu_loss_random_fwd compacts the pixel lists (pos_list /
+ * neg_list: #mask==1 / #mask==0 ints), gathers the 2n drawn pixels, writes
+ * the mean BCE and adds each drawn pixel's draw count into counts_px
+ * (n_pred ints, zeroed by the caller) for hcu_loss_ext_bwd(mode 6). */
+int hcu_loss_random_rows(int64_t n_pred);
+int hcu_loss_random_count(const float *pred, int B, int C, int PX, int PY, int PZ,
+                          const void *mask, int mask_dtype, int MX, int MY, int MZ,
+                          int *counts, hcu_stream_t stream);
+int hcu_loss_random_fwd(const float *pred, int B, int C, int PX, int PY, int PZ,
+                        const void *mask, int mask_dtype, int MX, int MY, int MZ,
+                        const int *offsets, int *pos_list, int *neg_list,
+                        const int64_t *pos_ind, const int64_t *neg_ind, int n,
+                        int *counts_px, float *loss, float *aux, void *scratch,
+                        size_t scratch_bytes, hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Optimizer.  Replaces torch.optim.Adam.step (tests/r_unet_test.py:24,56)   */
 /* for a flat parameter buffer: m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;  */
 /* p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps); L2 weight decay.     */
