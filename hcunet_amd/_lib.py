@@ -18,7 +18,7 @@ HCU_ERR_HIP = 3
 HCU_ERR_UNSUPPORTED = 4
 HCU_ERR_WORKSPACE = 5
 
-HCU_F32, HCU_F16, HCU_U8, HCU_BF16 = 0, 1, 2, 3
+HCU_F32, HCU_F16, HCU_U8, HCU_BF16, HCU_U16, HCU_F64 = 0, 1, 2, 3, 4, 5
 HCU_PLAN_FORWARD_ONLY = 1
 HCU_TILE_BATCH_MAX = 64
 MAX_LEVELS = 12
@@ -105,6 +105,8 @@ SYMBOLS = [
     ("hcu_loss_random_count", _I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _I, _VP, _VP]),
     ("hcu_loss_random_fwd", _I, [_VP, _I, _I, _I, _I, _I, _VP, _I, _I, _I, _I, _VP, _VP, _VP, _VP, _VP,
                                  _I, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    ("hcu_ingest_volume", _I, [_VP, _I, _I, _I, _I, _I, _I, _I, _I, ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double), _VP, _VP]),
     ("hcu_adam_step", _I, [_VP, _VP, _VP, _VP, _I64, _F, _F, _F, _F, _F, _I64, _F, _VP]),
     ("hcu_conv_scratch_bytes", _SZ, [ctypes.POINTER(ConvDesc)]),
     ("hcu_conv_out_dims", _I, [ctypes.POINTER(ConvDesc), ctypes.POINTER(_I)]),

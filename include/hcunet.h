@@ -57,7 +57,7 @@ enum {
   HCU_ERR_WORKSPACE = 5    /* workspace too small */
 };
 
-enum { HCU_F32 = 0, HCU_F16 = 1, HCU_U8 = 2, HCU_BF16 = 3 };
+enum { HCU_F32 = 0, HCU_F16 = 1, HCU_U8 = 2, HCU_BF16 = 3, HCU_U16 = 4, HCU_F64 = 5 };
 
 const char *hcu_last_error(void);
 int hcu_version(void);
@@ -217,6 +217,21 @@ int hcu_loss_random_fwd(const float *pred, int B, int C, int PX, int PY, int PZ,
                         const int64_t *pos_ind, const int64_t *neg_ind, int n,
                         int *counts_px, float *loss, float *aux, void *scratch,
                         size_t scratch_bytes, hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Input path.  Replaces, for B raw volumes at once, the     */
+/* reference's to_float (hcat/transforms.py:94-116) -> reshape (:139-157)    */
+/* -> normalize (:257-283) -> to_tensor (:118-137) chain: src [B][Z][Y][X][C] */
+/* of src_dtype HCU_U16 / HCU_U8 / HCU_F64; to_float: scale by 2^-16 / 2^-8; */
+/* reshape: output [B][C][X][Y][Z] (else [B][C][Z][Y][X]); mean/std (host    */
+/* arrays of C doubles, nullable): (v + -mean) / std.  Arithmetic in float64, */
+/* one round-to-nearest-even to fp16: bit-identical to the reference.  dst:  */
+/* fp16.  Fails with HCU_ERR_INVALID for other dtypes (the reference's       */
+/* TypeError, :113-114).                                                      */
+/* ------------------------------------------------------------------------ */
+int hcu_ingest_volume(const void *src, int src_dtype, int B, int Z, int Y, int X, int C,
+                      int to_float, int reshape, const double *mean, const double *std,
+                      void *dst, hcu_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Optimizer.  Replaces torch.optim.Adam.step (tests/r_unet_test.py:24,56)   */
