@@ -237,6 +237,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    t_enq = time.perf_counter() - t0   # host time to enqueue the K steps
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -295,7 +296,8 @@ def main():
                 "config": {"workload": "%s train step (fwd + pixel BCE + bwd + Adam), B=%d per "
                                        "GPU, %dx%dx%dx4 volumes" % ((cfg['desc'], B) + TILE),
                            "global_batch": B * world, "per_gpu_batch": B,
-                           "parallelism": "dp%d" % world, "final_loss": final_loss},
+                           "parallelism": "dp%d" % world, "final_loss": final_loss,
+                           "host_enqueue_ms_per_step": t_enq / args.steps * 1e3},
                 "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
         if cfg.get('roof_ms'):
             # SURVEY §8d per-layer roofline of the whole step (sum over layers of

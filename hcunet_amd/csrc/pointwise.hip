@@ -54,6 +54,37 @@ __device__ __forceinline__ float comp(const float4 &v, int j) {
   return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
 
+// 16-byte channel vectors: 4 fp32 or 8 bf16 channels per thread.
+template <typename T>
+struct VN {
+  static constexpr int N = 4;
+};
+template <>
+struct VN<bf16_t> {
+  static constexpr int N = 8;
+};
+__device__ __forceinline__ void ldv(const float *p, float (&f)[4]) {
+  const float4 v = ld4(p);
+  f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+}
+__device__ __forceinline__ void ldv(const bf16_t *p, float (&f)[8]) {
+  unpack8(*reinterpret_cast<const uint4 *>(p), f);
+}
+__device__ __forceinline__ void stv(float *p, const float (&f)[4]) {
+  st4(p, make_float4(f[0], f[1], f[2], f[3]));
+}
+__device__ __forceinline__ void stv(bf16_t *p, const float (&f)[8]) {
+  *reinterpret_cast<uint4 *>(p) = pack8(f);
+}
+template <int N>
+__device__ __forceinline__ void ldc(const float *p, float (&f)[N]) {   // fp32 coefficients
+#pragma unroll
+  for (int k = 0; k < N; k += 4) {
+    const float4 v = ld4(p + k);
+    f[k] = v.x; f[k + 1] = v.y; f[k + 2] = v.z; f[k + 3] = v.w;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // BatchNorm forward finalisation: one workgroup per channel.
 //
@@ -252,6 +283,53 @@ maxpool_fwd_kernel(const T *y, const float *scale, const float *shift, T *p,
   }
 }
 
+// MaxPool3d (2,2,1) on relu(bn(y)): one (window, 16-byte channel vector) per
+// thread, the window's 4 vectors loaded together.
+template <typename T>
+__global__ void __launch_bounds__(256)
+maxpool221_kernel(const T *y, const float *scale, const float *shift, T *p, int X, int Y, int Z,
+                  int Cs, int PX, int PY, uint32_t n, PoolDiv dv) {
+  constexpr int N = VN<T>::N;
+  const uint32_t idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n) return;
+  int v, g, pz, py, px, b;
+  dv.c4.divmod(idx, v, g);
+  dv.pz.divmod((uint32_t)v, v, pz);
+  dv.py.divmod((uint32_t)v, v, py);
+  dv.px.divmod((uint32_t)v, b, px);
+  const int c = g * N;
+  const size_t sy = (size_t)Z * Cs, sx = (size_t)Y * sy;
+  const size_t base = (((size_t)b * X + 2 * px) * Y + 2 * py) * sy + (size_t)pz * Cs + c;
+  float a[4][N];
+  ldv(y + base, a[0]);
+  ldv(y + base + sy, a[1]);
+  ldv(y + base + sx, a[2]);
+  ldv(y + base + sx + sy, a[3]);
+  float m[N];
+  if (scale) {
+    float sc[N], sh[N];
+    ldc<N>(scale + c, sc);
+    ldc<N>(shift + c, sh);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      m[j] = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float q = bnrelu(a[t][j], sc[j], sh[j]);
+        m[j] = q > m[j] ? q : m[j];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      m[j] = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) m[j] = a[t][j] > m[j] ? a[t][j] : m[j];
+    }
+  }
+  stv(p + ((((size_t)b * PX + px) * PY + py) * Z + pz) * Cs + c, m);
+}
+
 static int grid_for(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8192));
 }
@@ -271,6 +349,18 @@ int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
   const int PX = X / kx, PY = Y / ky, PZ = Z / kz;
   const int64_t n = (int64_t)B * PX * PY * PZ * (Cs / 4);
   if (n >= (int64_t)1 << 31) return fail(4, "max_pool3d: more than 2^31 channel quads per launch");
+  if (kx == 2 && ky == 2 && kz == 1 && n > 0) {
+    const int N = bf ? 8 : 4;
+    if (Cs % N == 0) {
+      const int64_t nv = (int64_t)B * PX * PY * PZ * (Cs / N);
+      HCU_TIMED(s, "maxpool221_kernel", 0.0, 0.0,
+                HCU_BF_DISPATCH(bf, maxpool221_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s,
+                                (const T *)y, scale, shift, (T *)p, X, Y, Z, Cs, PX, PY, (uint32_t)nv,
+                                pool_div(Cs * 4 / N, PX, PY, PZ)));
+      HCU_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   HCU_TIMED(s, "maxpool_fwd_kernel", 0.0, 0.0,
             HCU_BF_DISPATCH(bf, maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s,
                             (const T *)y, scale, shift, (T *)p, B, X, Y, Z, Cs, kx, ky, kz, PX,
@@ -448,6 +538,121 @@ bn_bwd_reduce_pool_kernel(const T *dP, const T *y, BNCoef coef, T *dz,
   block_reduce_c4<8>(v, lds, g.tb, C4, part + (size_t)blockIdx.x * Cs * 2);
 }
 
+// The same for MaxPool3d (2,2,1) with 16-byte channel vectors (4 fp32 / 8
+// bf16 channels) and two windows per iteration: the 2 x (4 + 1) vector loads
+// are issued together.  Per-thread channel group fixed (tb multiple of G);
+// accumulation order per channel is the generic kernel's (window order, then
+// the window's taps x-major), so partial rows are reproducible.
+template <int N>
+struct Win221 {
+  float a[4][N], gp[N];
+  int wx, wy, wz, b;
+  bool ok;
+};
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_pool221_kernel(const T *dP, const T *y, BNCoef coef, T *dz, int X, int Y, int Z,
+                             int Cs, float *part, RedGeom g, PoolDiv dv) {
+  constexpr int N = VN<T>::N;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int G = Cs / N, tid = threadIdx.x;
+  const int PX = X / 2, PY = Y / 2;
+  const size_t sy = (size_t)Z * Cs, sx = (size_t)Y * sy;
+  float v[2 * N];
+#pragma unroll
+  for (int k = 0; k < 2 * N; ++k) v[k] = 0.f;
+  if (tid < g.tb) {
+    const int64_t beg = (int64_t)blockIdx.x * g.chunk;
+    const int64_t end = std::min(beg + g.chunk, g.total);
+    const int c = (int)((beg + tid) % G) * N;
+    float sc[N], sh[N], mu[N], is[N];
+    ldc<N>(coef.scale + c, sc);
+    ldc<N>(coef.shift + c, sh);
+    ldc<N>(coef.mean + c, mu);
+    ldc<N>(coef.invstd + c, is);
+    auto load = [&](int64_t e, Win221<N> &w) {
+      w.ok = e < end;
+      if (!w.ok) return;
+      int q, gg;
+      dv.c4.divmod((uint32_t)e, q, gg);
+      dv.pz.divmod((uint32_t)q, q, w.wz);
+      dv.py.divmod((uint32_t)q, q, w.wy);
+      dv.px.divmod((uint32_t)q, w.b, w.wx);
+      const size_t base = (((size_t)w.b * X + 2 * w.wx) * Y + 2 * w.wy) * sy + (size_t)w.wz * Cs + c;
+      ldv(y + base, w.a[0]);
+      ldv(y + base + sy, w.a[1]);
+      ldv(y + base + sx, w.a[2]);
+      ldv(y + base + sx + sy, w.a[3]);
+      ldv(dP + ((((size_t)w.b * PX + w.wx) * PY + w.wy) * Z + w.wz) * Cs + c, w.gp);
+    };
+    auto finish = [&](const Win221<N> &w) {
+      if (!w.ok) return;
+      float d[4][N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        float m = -INFINITY;
+        int am = -1;
+        float zz[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          zz[t] = fmaf(w.a[t][j], sc[j], sh[j]);
+          const float q = fmaxf(zz[t], 0.f);
+          if (q > m) { m = q; am = t; }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) d[t][j] = (am == t && zz[t] > 0.f) ? w.gp[j] : 0.f;
+      }
+      const size_t base = (((size_t)w.b * X + 2 * w.wx) * Y + 2 * w.wy) * sy + (size_t)w.wz * Cs + c;
+      stv(dz + base, d[0]);
+      stv(dz + base + sy, d[1]);
+      stv(dz + base + sx, d[2]);
+      stv(dz + base + sx + sy, d[3]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          v[2 * j] += d[t][j];
+          v[2 * j + 1] = fmaf(d[t][j], (w.a[t][j] - mu[j]) * is[j], v[2 * j + 1]);
+        }
+      // floor mode: the last row / column of windows also owns the dropped voxels (gradient 0)
+      const bool lx = w.wx == PX - 1 && X > 2 * PX, ly = w.wy == PY - 1 && Y > 2 * PY;
+      if (lx || ly) {
+        float zero[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) zero[j] = 0.f;
+        const int x1 = lx ? X : 2 * w.wx + 2, y1 = ly ? Y : 2 * w.wy + 2;
+        for (int x = 2 * w.wx; x < x1; ++x)
+          for (int yy = 2 * w.wy; yy < y1; ++yy)
+            if (x >= 2 * w.wx + 2 || yy >= 2 * w.wy + 2)
+              stv(dz + (((size_t)w.b * X + x) * Y + yy) * sy + (size_t)w.wz * Cs + c, zero);
+      }
+    };
+    for (int64_t e = beg + tid; e < end; e += 2 * (int64_t)g.tb) {
+      Win221<N> w0, w1;
+      load(e, w0);
+      load(e + g.tb, w1);
+      finish(w0);
+      finish(w1);
+    }
+  }
+  // fixed-order reduction per channel group -> part[row][c][2]
+  if (tid < g.tb)
+#pragma unroll
+    for (int k = 0; k < 2 * N; ++k) lds[tid * 2 * N + k] = v[k];
+  __syncthreads();
+  if (tid < G) {
+    float acc[2 * N];
+#pragma unroll
+    for (int k = 0; k < 2 * N; ++k) acc[k] = 0.f;
+    for (int t = tid; t < g.tb; t += G)
+#pragma unroll
+      for (int k = 0; k < 2 * N; ++k) acc[k] += lds[t * 2 * N + k];
+    float *out = part + (size_t)blockIdx.x * Cs * 2 + (size_t)tid * 2 * N;
+#pragma unroll
+    for (int k = 0; k < 2 * N; ++k) out[k] = acc[k];
+  }
+}
+
 int pool_bwd_rows(int B, int X, int Y, int Z, int Cs, int kx, int ky, int kz) {
   return bwd_rows((int64_t)B * (X / kx) * (Y / ky) * (Z / kz), Cs);
 }
@@ -457,6 +662,17 @@ int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, floa
                               int kz, float *part, int R, hipStream_t s, int bf) {
   const RedGeom g = red_geom((int64_t)B * (X / kx) * (Y / ky) * (Z / kz), Cs, R);
   if (g.total >= (int64_t)1 << 31) return fail(4, "max_pool3d backward: more than 2^31 channel quads");
+  const int N = bf ? 8 : 4;
+  if (kx == 2 && ky == 2 && kz == 1 && Cs % N == 0) {
+    // red_geom over N-channel groups: pass Cs * 4 / N as the "quad" stride
+    const RedGeom gv = red_geom((int64_t)B * (X / 2) * (Y / 2) * Z, Cs * 4 / N, R);
+    HCU_TIMED(s, "bn_bwd_reduce_pool221_kernel", 0.0, 0.0,
+              HCU_BF_DISPATCH(bf, bn_bwd_reduce_pool221_kernel, dim3(R), dim3(256),
+                              (size_t)std::max(gv.tb, 256) * 2 * N * 4, s, (const T *)dP, (const T *)y,
+                              coef, (T *)dz, X, Y, Z, Cs, part, gv, pool_div(Cs * 4 / N, X / 2, Y / 2, Z)));
+    HCU_CHECK_LAUNCH();
+    return 0;
+  }
   HCU_TIMED(s, "bn_bwd_reduce_pool_kernel", 0.0, 0.0,
             HCU_BF_DISPATCH(bf, bn_bwd_reduce_pool_kernel, dim3(R), dim3(256),
                             (size_t)std::max(g.tb, 256) * 8 * 4, s, (const T *)dP, (const T *)y,
@@ -498,8 +714,64 @@ bn_bwd_apply_kernel(T *dz, const T *y, BNCoef coef, int64_t n4, int C4) {
   for (; i < n4; i += st) st4(dz + i * 4, f(ld4(dz + i * 4), ld4(y + i * 4)));
 }
 
+// The same with 16-byte channel vectors (8 bf16 channels per load on the bf16
+// path), 4 vectors in flight per thread.
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_vec_kernel(T *dz, const T *y, BNCoef coef, int64_t nv, int G) {
+  constexpr int N = VN<T>::N;
+  const int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t st = (int64_t)gridDim.x * 256;
+  const int c = (int)(i0 % G) * N;
+  float sc[N], c1[N], c0[N];
+  ldc<N>(coef.scale + c, sc);
+  ldc<N>(coef.c1 + c, c1);
+  ldc<N>(coef.c0 + c, c0);
+  int64_t i = i0;
+  for (; i + 3 * st < nv; i += 4 * st) {
+    float yy[4][N], d[4][N];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      ldv(y + (i + u * st) * N, yy[u]);
+      ldv(dz + (i + u * st) * N, d[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) d[u][j] = fmaf(d[u][j], sc[j], fmaf(c1[j], yy[u][j], c0[j]));
+      stv(dz + (i + u * st) * N, d[u]);
+    }
+  }
+  for (; i < nv; i += st) {
+    float yy[N], d[N];
+    ldv(y + i * N, yy);
+    ldv(dz + i * N, d);
+#pragma unroll
+    for (int j = 0; j < N; ++j) d[j] = fmaf(d[j], sc[j], fmaf(c1[j], yy[j], c0[j]));
+    stv(dz + i * N, d);
+  }
+}
+
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, int Cs,
                         hipStream_t s, int bf) {
+  {
+    const int N = bf ? 8 : 4;
+    if (Cs % N == 0) {
+      const int G = Cs / N;
+      const int64_t nv = nvox * G;
+      int64_t want = (nv + 1023) / 1024;   // ~4 vectors per thread
+      int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, 65536));
+      if (256 % G) {
+        const int per = G / std::__gcd(256, G);
+        grid = std::max(per, grid / per * per);
+      }
+      HCU_TIMED(s, "bn_bwd_apply_vec_kernel", 0.0, 0.0,
+                HCU_BF_DISPATCH(bf, bn_bwd_apply_vec_kernel, dim3(grid), dim3(256), 0, s, (T *)dz,
+                                (const T *)y, coef, nv, G));
+      HCU_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   const int64_t n4 = nvox * (Cs / 4);
   const int C4 = Cs / 4;
   // grid * 256 must be a multiple of C4 (fixed channel quad per thread)
@@ -723,6 +995,22 @@ to_cl_kernel(const TI *x, T *xcl, int B, int C, int Cs, int64_t V, FastDiv fV, F
   }
 }
 
+// One voxel per thread for the network input (C <= 8, Cs = 4 fp32 / 8 bf16):
+// C coalesced plane loads, one 16-byte channels-last store.
+template <typename TI, typename T>
+__global__ void __launch_bounds__(256)
+to_cl_vox_kernel(const TI *x, T *xcl, int C, int64_t V, uint32_t n, FastDiv fV) {
+  constexpr int N = VN<T>::N;
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int b, v;
+  fV.divmod(i, b, v);
+  float r[N];
+#pragma unroll
+  for (int c = 0; c < N; ++c) r[c] = c < C ? ld1(x + ((size_t)b * C + c) * V + v) : 0.f;
+  stv(xcl + (size_t)i * N, r);
+}
+
 // x_dtype: HCU_F32 / HCU_F16 / 3 = bf16 input volume; bf: bf16 channels-last output.
 int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s,
                  int bf, int x_dtype) {
@@ -730,6 +1018,34 @@ int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hi
   if (n >= (int64_t)1 << 31) return fail(4, "input volume: more than 2^31 channel quads");
   const dim3 gr(grid_for(n));
   const FastDiv fV((uint32_t)V), fC4((uint32_t)(Cs / 4));
+  if (Cs == (bf ? 8 : 4) && C <= Cs && (int64_t)B * V < ((int64_t)1 << 31)) {
+    const uint32_t nv = (uint32_t)(B * V);
+    const dim3 g2((nv + 255) / 256);
+    if (x_dtype == 1 && bf)
+      HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
+                hipLaunchKernelGGL((to_cl_vox_kernel<_Float16, bf16_t>), g2, dim3(256), 0, s,
+                                   (const _Float16 *)x, (bf16_t *)xcl, C, V, nv, fV));
+    else if (x_dtype == 3 && bf)
+      HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
+                hipLaunchKernelGGL((to_cl_vox_kernel<bf16_t, bf16_t>), g2, dim3(256), 0, s,
+                                   (const bf16_t *)x, (bf16_t *)xcl, C, V, nv, fV));
+    else if (x_dtype == 0 && bf)
+      HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
+                hipLaunchKernelGGL((to_cl_vox_kernel<float, bf16_t>), g2, dim3(256), 0, s, x,
+                                   (bf16_t *)xcl, C, V, nv, fV));
+    else if (x_dtype == 1)
+      HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
+                hipLaunchKernelGGL((to_cl_vox_kernel<_Float16, float>), g2, dim3(256), 0, s,
+                                   (const _Float16 *)x, xcl, C, V, nv, fV));
+    else if (x_dtype == 0)
+      HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
+                hipLaunchKernelGGL((to_cl_vox_kernel<float, float>), g2, dim3(256), 0, s, x, xcl, C, V,
+                                   nv, fV));
+    else
+      return fail(4, "to_cl: unsupported input dtype");
+    HCU_CHECK_LAUNCH();
+    return 0;
+  }
   if (x_dtype == 1 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<_Float16, bf16_t>), gr, dim3(256), 0, s,

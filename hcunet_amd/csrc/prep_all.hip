@@ -38,58 +38,66 @@ __device__ __forceinline__ float weff2(const float *w, int o, int e, int t, int 
   return s;
 }
 
-__device__ float prep_value(const PrepJob &jb, const float *w, uint32_t i) {
+// Index decoding of the packed jobs: image element i -> (t, a, b), where `a`
+// (the middle index) advances by one across the V = 8 (bf16) / 4 (fp32)
+// consecutive elements of one packed vector (wpack_decode's j).
+__device__ __forceinline__ bool prep_decode(const PrepJob &jb, uint32_t i, int &t, int &a, int &b) {
   const int *p = jb.p;
   switch (jb.kind) {
-    case PREP_CONV_FWD: {
-      int t, e, co;
-      if (prep_index2(jb.pk, i, p[4], p[5], p[6], t, e, co) && co < p[0] && e < p[7])
-        return weff2(w, co, e, t, p[0], p[1], p[2], p[3], p[4]);
-      return 0.f;
-    }
-    case PREP_CONV_DGRAD: {
-      int tp, co, e;
-      if (prep_index2(jb.pk, i, p[4], p[5], p[6], tp, co, e) && co < p[0] && e < p[7])
-        return weff2(w, co, e, p[4] - 1 - tp, p[0], p[1], p[2], p[3], p[4]);
-      return 0.f;
-    }
+    case PREP_CONV_FWD:
+    case PREP_CONV_DGRAD:
+      return prep_index2(jb.pk, i, p[4], p[5], p[6], t, a, b);
     case PREP_CONVT_FUSED: {
+      const int T = (p[2] / p[5]) * (p[3] / p[6]) * (p[4] / p[7]);
+      return prep_index2(jb.pk, i, T, p[8], p[9], t, a, b);
+    }
+    default:   // PREP_CONVT_DGRAD
+      return prep_index2(jb.pk, i, p[2], p[3], p[4], t, a, b);
+  }
+}
+
+// Value of a decoded (t, a, b) element (0 for padding).
+__device__ __forceinline__ float prep_eval(const PrepJob &jb, const float *w, int t, int a, int b) {
+  const int *p = jb.p;
+  switch (jb.kind) {
+    case PREP_CONV_FWD:   // (t, e, co)
+      return (b < p[0] && a < p[7]) ? weff2(w, b, a, t, p[0], p[1], p[2], p[3], p[4]) : 0.f;
+    case PREP_CONV_DGRAD:   // (t', co, e)
+      return (a < p[0] && b < p[7]) ? weff2(w, a, b, p[4] - 1 - t, p[0], p[1], p[2], p[3], p[4]) : 0.f;
+    case PREP_CONVT_FUSED: {   // (t, ci, nn)
       const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
       const int sx = p[5], sy = p[6], sz = p[7];
       const int Jx = KX / sx, Jy = KY / sy, Jz = KZ / sz;
-      const int T = Jx * Jy * Jz;
-      int t, ci, nn;
-      if (prep_index2(jb.pk, i, T, p[8], p[9], t, ci, nn) && ci < Cin && nn < sx * sy * sz * Cout) {
-        const int ph = nn / Cout, co = nn % Cout;
-        const int qz = ph % sz, qy = (ph / sz) % sy, qx = ph / (sz * sy);
-        const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
-        const int kx = qx + sx * (Jx - 1 - tx), ky = qy + sy * (Jy - 1 - ty),
-                  kz = qz + sz * (Jz - 1 - tz);
-        return w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
-      }
-      return 0.f;
-    }
-    case PREP_CONVT_PHASE: {
-      const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
-      const int Jx = p[11], Jy = p[12], Jz = p[13], ICs = p[14], CoutW = p[15];
-      const int co = (int)(i % (uint32_t)CoutW);
-      const uint32_t q = i / (uint32_t)CoutW;
-      const int ci = (int)(q % (uint32_t)ICs);
-      const int t = (int)(q / (uint32_t)ICs);
+      if (a >= Cin || b >= sx * sy * sz * Cout) return 0.f;
+      const int ph = b / Cout, co = b % Cout;
+      const int qz = ph % sz, qy = (ph / sz) % sy, qx = ph / (sz * sy);
       const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
-      const int kx = p[8] + p[5] * (Jx - 1 - tx), ky = p[9] + p[6] * (Jy - 1 - ty),
-                kz = p[10] + p[7] * (Jz - 1 - tz);
-      if (ci < Cin && co < Cout && kx < KX && ky < KY && kz < KZ)
-        return w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
-      return 0.f;
+      const int kx = qx + sx * (Jx - 1 - tx), ky = qy + sy * (Jy - 1 - ty), kz = qz + sz * (Jz - 1 - tz);
+      return w[((((size_t)a * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
     }
-    default: {  // PREP_CONVT_DGRAD
-      int t, co, ci;
-      if (prep_index2(jb.pk, i, p[2], p[3], p[4], t, co, ci) && ci < p[0] && co < p[1])
-        return w[((size_t)ci * p[1] + co) * p[2] + t];
-      return 0.f;
-    }
+    default:   // PREP_CONVT_DGRAD: (t, co, ci)
+      return (b < p[0] && a < p[1]) ? w[((size_t)b * p[1] + a) * p[2] + t] : 0.f;
   }
+}
+
+__device__ float prep_value(const PrepJob &jb, const float *w, uint32_t i) {
+  if (jb.kind == PREP_CONVT_PHASE) {
+    const int *p = jb.p;
+    const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
+    const int Jx = p[11], Jy = p[12], Jz = p[13], ICs = p[14], CoutW = p[15];
+    const int co = (int)(i % (uint32_t)CoutW);
+    const uint32_t q = i / (uint32_t)CoutW;
+    const int ci = (int)(q % (uint32_t)ICs);
+    const int t = (int)(q / (uint32_t)ICs);
+    const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
+    const int kx = p[8] + p[5] * (Jx - 1 - tx), ky = p[9] + p[6] * (Jy - 1 - ty),
+              kz = p[10] + p[7] * (Jz - 1 - tz);
+    if (ci < Cin && co < Cout && kx < KX && ky < KY && kz < KZ)
+      return w[((((size_t)ci * Cout + co) * KX + kx) * KY + ky) * KZ + kz];
+    return 0.f;
+  }
+  int t, a, b;
+  return prep_decode(jb, i, t, a, b) ? prep_eval(jb, w, t, a, b) : 0.f;
 }
 
 __global__ void __launch_bounds__(256)
@@ -98,6 +106,37 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
   const float *w = params + jb.src;
   float *dst = dst_base + jb.dst;
   const uint32_t n = (uint32_t)jb.n;   // < 2^31 (launch_prep_all)
+  // packed images: one decode per 16-byte vector (8 bf16 / 4 fp32 elements
+  // whose middle index advances by one), one 16-byte store
+  if (jb.pk.on && jb.kind != PREP_CONVT_PHASE && ((uintptr_t)dst & 15) == 0) {
+    if (jb.bf16 && jb.pk.on == 3 && n % 8 == 0) {
+      uint4 *d = reinterpret_cast<uint4 *>(dst);
+      for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n / 8; k += gridDim.x * 256) {
+        int t, a, b;
+        const bool ok = prep_decode(jb, k * 8, t, a, b);
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = ok ? prep_eval(jb, w, t, a + j, b) : 0.f;
+        d[k] = make_uint4((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                          (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16),
+                          (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16),
+                          (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16));
+      }
+      return;
+    }
+    if (!jb.bf16 && jb.pk.on != 3 && n % 4 == 0) {
+      float4 *d = reinterpret_cast<float4 *>(dst);
+      for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n / 4; k += gridDim.x * 256) {
+        int t, a, b;
+        const bool ok = prep_decode(jb, k * 4, t, a, b);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = ok ? prep_eval(jb, w, t, a + j, b) : 0.f;
+        d[k] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+      return;
+    }
+  }
   if (jb.bf16) {
     uint16_t *d16 = reinterpret_cast<uint16_t *>(dst);
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)

@@ -85,6 +85,19 @@ def main():
           % (mq, tot, len(ks), tot / max(1, len(ks))))
     for g, p, n in sorted(gaps, key=lambda x: -x[0])[:a.gaps]:
         print('  gap %7.1f us  after %-48s before %s' % (g, short(p), short(n)))
+    # stream attribution by kernel family: the weight-gradient branch runs on
+    # the executor's side stream
+    side_keys = ('wgrad', 'chansum', 'reduce_partials', 'outconv_wfinalize')
+    main_ev = [(s_, e_, n) for n, s_, e_, _ in step if not any(k in n for k in side_keys)]
+    side_ev = [(s_, e_, n) for n, s_, e_, _ in step if any(k in n for k in side_keys)]
+    if side_ev:
+        bwd0 = min(s_ for s_, _, n in side_ev)
+        mb = [(s_, e_, n) for s_, e_, n in main_ev if s_ >= bwd0 and 'adam' not in n]
+        print('backward from first side-stream kernel: main busy %.1f us (ends at +%.1f), side busy %.1f us '
+              '(ends at +%.1f), adam starts at +%.1f'
+              % (sum(e_ - s_ for s_, e_, _ in mb) / 1e3, (max(e_ for _, e_, _ in mb) - bwd0) / 1e3 if mb else 0,
+                 sum(e_ - s_ for s_, e_, _ in side_ev) / 1e3, (max(e_ for _, e_, _ in side_ev) - bwd0) / 1e3,
+                 (max(s_ for s_, _, n in main_ev if 'adam' in n) - bwd0) / 1e3))
     print('\ncritical-queue sequence (us: start offset, duration):')
     for n, s, e in ks:
         print('  %8.1f %7.1f  %s' % ((s - t0) / 1e3, (e - s) / 1e3, short(n)))
