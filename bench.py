@@ -263,7 +263,7 @@ def main():
         avg_s = d['ms'] / d['count'] / 1e3
         if d['flops'] > 0:
             ach = d['flops'] / d['count'] / avg_s / 1e12
-            bf_kernel = name.startswith(('bconv', 'bwgrad'))
+            bf_kernel = 'bf16' in name or name.startswith('bwgrad')   # bconv_kernel<f32,...> is fp32
             bound, unit = 'mfma', 'TFLOP/s'
             peak = PEAK_BF16_MFMA_TFLOPS if bf_kernel else PEAK_FP32_MFMA_TFLOPS
         else:
