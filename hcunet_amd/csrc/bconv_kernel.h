@@ -623,6 +623,13 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     else
       *reinterpret_cast<float2 *>(a.stats + c * 2) = make_float2(S1, S2);
   }
+  if (fwdstat && a.fin.counter) {   // fused BatchNorm finalize (BnFin, common.h)
+    __syncthreads();
+    if (bn_fin_ticket(a.fin.counter, reinterpret_cast<int *>(smem))) {
+      bn_fwd_finalize_tail(a.stats, a.fin, reinterpret_cast<double *>(smem));
+      if (tid == 0) *a.fin.counter = 0u;
+    }
+  }
 #undef KA
 }
 
@@ -736,6 +743,14 @@ __global__ void __launch_bounds__(256) bconv_reduce_kernel(const GConvArgs a, in
             make_float4(t1, t2, piv[k], tn);
       else
         *reinterpret_cast<float2 *>(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 2) = make_float2(t1, t2);
+    }
+  }
+  if (fwdstat && a.fin.counter) {   // fused BatchNorm finalize (BnFin, common.h)
+    __shared__ double fred[768];
+    __shared__ int fflag;
+    if (bn_fin_ticket(a.fin.counter, &fflag)) {
+      bn_fwd_finalize_tail(a.stats, a.fin, fred);
+      if (tid == 0) *a.fin.counter = 0u;
     }
   }
 }

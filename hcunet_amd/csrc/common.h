@@ -139,6 +139,24 @@ int fail(int code, const std::string &msg);
 // taps), ConvTranspose3d dgrad (strided) and ConvTranspose3d forward (one
 // launch per output phase).  Optional per-block BatchNorm partial statistics.
 // ---------------------------------------------------------------------------
+struct BNCoef {
+  float *scale, *shift, *mean, *invstd, *c1, *c0;  // [Cs] each
+};
+// Forward BatchNorm finalize fused into the producing convolution (training):
+// every workgroup writes its statistics row, then takes a ticket from
+// `counter`; the workgroup holding the last ticket combines all R rows in
+// fp64 (bn_fwd_finalize_tail) into the layer's coefficients and running
+// statistics, and resets the counter to 0.  counter == nullptr: not fused.
+struct BnFin {
+  const float *gamma, *beta;
+  float *rm, *rv;
+  const int64_t *nbt;
+  BNCoef coef;
+  double count;
+  float eps, momentum;
+  int C, Cs, R, W;
+  unsigned *counter;
+};
 struct GConvArgs {
   const float *in;
   const float *in_scale, *in_shift;   // [ICs] or null
@@ -185,7 +203,112 @@ struct GConvArgs {
   // (channels-last activations, packed weights); partial stays fp32.
   int use_bconv;
   int bes;   // bconv element bytes: 2 (bf16 activations) or 4 (fp32); 0 = 2
+  BnFin fin;   // bconv forward with statistics: fused BatchNorm finalize
 };
+
+// The last-workgroup BatchNorm forward finalize (256 threads, `red` = 768
+// doubles of LDS).  One pass over the R statistics rows: TPC threads per
+// channel each merge a strided subset of rows by the parallel-variance
+// (Chan) update of (n, mean, M2), loads issued 8 rows at a time; the TPC
+// partial states are then merged in a fixed tree order.  fp64 throughout,
+// deterministic (same rows, same order every run).
+__device__ __forceinline__ void chan_merge(double &n, double &mu, double &m2, double nb, double mub,
+                                           double m2b) {
+  if (nb <= 0.0) return;
+  if (n <= 0.0) {
+    n = nb; mu = mub; m2 = m2b;
+    return;
+  }
+  const double nn = n + nb, d = mub - mu;
+  mu += d * (nb / nn);
+  m2 += m2b + d * d * (n * nb / nn);
+  n = nn;
+}
+__device__ __forceinline__ void bn_fwd_finalize_tail(const float *stats, const BnFin &f, double *red) {
+  const int tid = threadIdx.x;
+  int TPC = 1;
+  while (TPC * 2 * f.C <= 256 && TPC < 64) TPC *= 2;
+  const int CPP = 256 / TPC, sub = tid % TPC;
+  for (int c0 = 0; c0 < f.Cs; c0 += CPP) {
+    const int c = c0 + tid / TPC;
+    double n = 0.0, mu = 0.0, m2 = 0.0;
+    if (c < f.C) {
+      for (int r0 = sub; r0 < f.R; r0 += 8 * TPC) {
+        float4 row[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = r0 + u * TPC;
+          row[u] = r < f.R ? *reinterpret_cast<const float4 *>(stats + ((size_t)r * f.W + c) * 4)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (row[u].w > 0.f) {   // row: sums of (y - K), (y - K)^2 over n = w values
+            const double nr = row[u].w, s1 = row[u].x;
+            chan_merge(n, mu, m2, nr, (double)row[u].z + s1 / nr, (double)row[u].y - s1 * s1 / nr);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    red[tid] = n;
+    red[256 + tid] = mu;
+    red[512 + tid] = m2;
+    __syncthreads();
+    for (int off = TPC / 2; off > 0; off >>= 1) {
+      if (sub < off) {
+        double a = red[tid], b = red[256 + tid], q = red[512 + tid];
+        chan_merge(a, b, q, red[tid + off], red[256 + tid + off], red[512 + tid + off]);
+        red[tid] = a;
+        red[256 + tid] = b;
+        red[512 + tid] = q;
+      }
+      __syncthreads();
+    }
+    if (sub == 0 && c < f.Cs) {
+      if (c >= f.C) {
+        f.coef.scale[c] = f.coef.shift[c] = f.coef.mean[c] = f.coef.invstd[c] = 0.f;
+        f.coef.c1[c] = f.coef.c0[c] = 0.f;
+      } else {
+        const double m = red[256 + tid];
+        double v = red[512 + tid] / red[tid];
+        if (v < 0.0) v = 0.0;
+        const float mean = (float)m, invstd = (float)(1.0 / sqrt(v + (double)f.eps));
+        if (f.rm) {
+          const double fm = f.momentum >= 0.f ? (double)f.momentum : 1.0 / (double)(f.nbt[0] + 1);
+          const double unb = f.count > 1.0 ? v * f.count / (f.count - 1.0) : v;
+          f.rm[c] = (float)(fm * m + (1.0 - fm) * (double)f.rm[c]);
+          f.rv[c] = (float)(fm * unb + (1.0 - fm) * (double)f.rv[c]);
+        }
+        const float g = f.gamma ? f.gamma[c] : 1.f, bb = f.beta ? f.beta[c] : 0.f;
+        const float sc = g * invstd;
+        f.coef.scale[c] = sc;
+        f.coef.shift[c] = bb - mean * sc;
+        f.coef.mean[c] = mean;
+        f.coef.invstd[c] = invstd;
+      }
+    }
+  }
+}
+
+// Ticket of a workgroup that has written its statistics row; true for the last.
+// Writers publish with an agent-scope RELEASE fence only (L2 write-back, no
+// invalidate: a full __threadfence in every workgroup invalidates the XCD's
+// L2 under the still-running workgroups); the last one ACQUIREs.
+__device__ __forceinline__ bool bn_fin_ticket(unsigned *counter, int *flag_lds) {
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+    *flag_lds = atomicAdd(counter, 1u) == nb - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = *(volatile int *)flag_lds != 0;
+  __syncthreads();
+  if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return last;
+}
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
 // (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n
 // outputs the row's workgroup produced, K a pivot value taken from those
@@ -330,9 +453,6 @@ int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s);
 // Pointwise / reduction kernels (pointwise.hip)
 // ---------------------------------------------------------------------------
 // Per-layer BatchNorm coefficient block, each array padded to Cs with zeros.
-struct BNCoef {
-  float *scale, *shift, *mean, *invstd, *c1, *c0;  // [Cs] each
-};
 
 int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
                            double count, const float *gamma, const float *beta,

@@ -342,6 +342,7 @@ struct hcu_unet_plan {
   // layers later (see Ctx::alloc).
   size_t buf_off[HCU_NBUF] = {};
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
+  size_t fin_off = 0;   // fused BatchNorm finalize ticket counter (zeroed per forward)
   size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
   // Captured launch sequences (hipGraph) keyed by the buffers they bake in:
   // forward and backward are fixed kernel sequences, so a replay costs one
@@ -616,6 +617,7 @@ int build_plan(hcu_unet_plan &p) {
   p.wpart_off = scratch.take_floats(fwd_only ? 0 : p.max_part);
   p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
+  p.fin_off = scratch.take_floats(16);
   p.scratch_bytes = scratch.off;
   return 0;
 }
@@ -689,8 +691,31 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   a.out = c.fptr(c.sv, L.y_off);
   a.stats = training ? c.part() : nullptr;
   a.partial = c.kpart();
-  if (int e = launch_conv_any(a, c.s)) return e;
   const BNCoef coef = coef_at(c.sv, L.bn);
+  // training bconv, opt-in (HCU_BNFIN=1): the BatchNorm finalize in the conv's
+  // last workgroup.  Measured slower (+35..60 us per layer on MI355X: every
+  // workgroup's agent-scope release fence writes back its XCD's L2), so the
+  // separate finalize launch stays the default.
+  static const bool use_fin = getenv("HCU_BNFIN") && getenv("HCU_BNFIN")[0] == '1';
+  if (training && a.use_bconv && use_fin && a.lds_bytes - (int)sizeof(GConvArgs) >= 6144) {
+    BnFin &f = a.fin;
+    f.gamma = c.P + L.bn.gamma;
+    f.beta = c.P + L.bn.beta;
+    f.rm = c.t.bn_running_mean[L.bn.index];
+    f.rv = c.t.bn_running_var[L.bn.index];
+    f.nbt = c.t.bn_num_batches_tracked[L.bn.index];
+    f.coef = coef;
+    f.count = L.bn.count;
+    f.eps = c.p.spec.bn_eps;
+    f.momentum = c.p.spec.bn_momentum;
+    f.C = L.bn.C;
+    f.Cs = L.bn.Cs;
+    f.R = gconv_rows(L.fwd);
+    f.W = L.fwd.CoutW;
+    f.counter = reinterpret_cast<unsigned *>(c.fptr(c.sc, c.p.fin_off));
+    return launch_conv_any(a, c.s);
+  }
+  if (int e = launch_conv_any(a, c.s)) return e;
   return launch_bn_fwd_finalize(c.part(), gconv_rows(L.fwd), L.fwd.CoutW, L.bn.C, L.bn.Cs,
                                 L.bn.count, c.P + L.bn.gamma, c.P + L.bn.beta,
                                 c.t.bn_running_mean[L.bn.index], c.t.bn_running_var[L.bn.index],
@@ -950,6 +975,7 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
+  if (training) HCU_HIP(hipMemsetAsync(c.fptr(c.sc, p.fin_off), 0, 64, c.s));
   tag(std::string("in"), "fwd");
   if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
                            t->x_dtype))

@@ -62,3 +62,17 @@ def test_split_graphed_equals_serial(tmp_path):
     for it in range(3):
         for a, b in zip(serial[it], split[it]):
             assert torch.equal(a, b)
+
+
+def test_fused_bn_finalize_matches_separate(tmp_path):
+    """HCU_BNFIN=1 (opt-in): the forward BatchNorm finalize in the conv's last
+    workgroup (one-pass Chan merge) agrees with the separate finalize launch
+    (two-pass) to fp32 rounding of the coefficients, deterministically."""
+    sep = _run(tmp_path, 'sep', {})
+    fin1 = _run(tmp_path, 'fin1', {'HCU_BNFIN': '1'})
+    fin2 = _run(tmp_path, 'fin2', {'HCU_BNFIN': '1'})
+    for it in range(3):
+        for a, b, c in zip(sep[it], fin1[it], fin2[it]):
+            assert torch.equal(b, c)
+            tol = 1e-4 * max(a.abs().max().item(), 1e-6)
+            assert (a - b).abs().max().item() <= tol
