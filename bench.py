@@ -106,16 +106,62 @@ def cpu_baseline(cfg, x, mask, pwl, budget_s=15.0):
                       % (len(times), x.shape[0], threads, med)}
 
 
-def load_traffic(kernel):
+def tagify(rocprof_name):
+    """rocprofv3 kernel symbol -> the name bench.py's HIP-event timing uses
+    ("void hcu::bconv_kernel<float, 4, 1, 1, 4, false>(hcu::GConvArgs)" ->
+    "bconv_kernel<f32,4,1,1,4>"; element-type-only templates lose the <...>)."""
+    import re
+    n = re.sub(r'^void\s+', '', rocprof_name.strip())
+    n = re.sub(r'\(.*\)$', '', n).replace('hcu::', '').replace(' ', '')
+    if '<' in n:
+        args = n.split('<', 1)[1].rstrip('>').split(',')
+        if all(x in ('float', '_Float16', 'bf16_t', 'unsignedshort', 'double', 'unsignedchar') for x in args):
+            return n.split('<', 1)[0]   # element-type-only templates: timed under the base name
+    n = n.replace('<float,', '<f32,').replace('<unsignedshort,', '<bf16,')
+    n = n.replace(',false>', '>').replace(',true>', ',bnb>')
+    return n
+
+
+def load_traffic(kernel, config='2'):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/traffic.json, written by tools/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, 'profiles', 'traffic.json')
-    try:
-        with open(path) as f:
-            tab = json.load(f)
-        return tab.get(kernel, {}).get('hbm_bytes_per_launch')
-    except (OSError, ValueError):
+    tab = None
+    for fn in ('traffic_config%s.json' % config, 'traffic.json' if config == '2' else None):
+        if not fn:
+            continue
+        try:
+            with open(os.path.join(ROOT, 'profiles', fn)) as f:
+                tab = json.load(f)
+            break
+        except (OSError, ValueError):
+            continue
+    if tab is None:
         return None
+    tot, n = 0.0, 0
+    for k, v in tab.items():
+        if isinstance(v, dict) and tagify(k) == kernel:
+            tot += v['hbm_bytes_per_launch'] * v['launches']
+            n += v['launches']
+    return tot / n if n else None
+
+
+def rocprof_avg_us(kernel, config):
+    """Average duration (us) of `kernel` in the committed rocprofv3
+    --kernel-trace --stats summary of this config's graphed bench step
+    (profiles/r02_kernel_stats_config<config>.csv), or None."""
+    import csv
+    path = os.path.join(ROOT, 'profiles', 'r02_kernel_stats_config%s.csv' % config)
+    try:
+        with open(path, newline='') as f:
+            rows = list(csv.DictReader(f))
+    except OSError:
+        return None
+    tot, calls = 0.0, 0
+    for r in rows:
+        if tagify(r['Name']) == kernel:
+            tot += float(r['TotalDurationNs'])
+            calls += int(r['Calls'])
+    return tot / calls / 1e3 if calls else None
 
 
 # The network of the reference's inference pipeline (hcat/main.py:46-54) and
@@ -270,8 +316,9 @@ def main():
             ach = d['bytes'] / d['count'] / avg_s / 1e9
             bound, peak, unit = 'hbm', PEAK_HBM_GBS, 'GB/s'
         roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit,
-                    "frac": ach / peak, "traffic": load_traffic(name), "kernel": name,
+                    "frac": ach / peak, "traffic": load_traffic(name, args.config), "kernel": name,
                     "avg_launch_us": avg_s * 1e6,
+                    "rocprof_avg_launch_us": rocprof_avg_us(name, args.config),
                     "launches_per_step": d['count'] / args.steps,
                     "flops_per_launch": d['flops'] / d['count'],
                     "share_of_kernel_time": d['ms'] / total_ms}
