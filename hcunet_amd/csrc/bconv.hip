@@ -58,6 +58,11 @@ static void bconv_finish(GConvArgs &a, int ntz, int VEC, int fpf);
 // ---- measured planning: times a candidate on scratch buffers of its shapes
 static std::mutex g_tune_mu;
 static std::map<std::string, int> g_tune;
+// Measured planning is off while a forward-only (inference) plan is built: its
+// tile-batch size follows the free device memory, so every call can bring new
+// signatures, and timing those costs seconds per call.
+static thread_local bool g_tune_off = false;
+void bconv_tuning(bool on) { g_tune_off = !on; }
 
 static std::string bconv_signature(const GConvArgs &a) {
   const int v[] = {a.bes, a.B, a.IX, a.IY, a.IZ, a.ICs, a.OX, a.OY, a.OZ, a.SX, a.SY, a.SZ, a.OCs,
@@ -255,7 +260,10 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   // Measured choice among the model's best candidates (HCU_BCONV_TUNE=0: the
   // model's first choice), remembered per convolution signature.
   const int top = std::min<int>((int)cands.size(), env_int_b("HCU_BCONV_TUNE_TOP", 6));
-  if (env_int_b("HCU_BCONV_TUNE", 1) && top > 1 && !fck && !fns && !fmp) {
+  // Not for very large convolutions (~10^8 output voxels: seconds of timing)
+  // nor in forward-only plans (g_tune_off).
+  const double out_vox = (double)a.B * a.OX * a.OY * a.OZ;
+  if (env_int_b("HCU_BCONV_TUNE", 1) && top > 1 && !fck && !fns && !fmp && out_vox <= 16e6 && !g_tune_off) {
     const std::string key = bconv_signature(a);
     std::lock_guard<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);

@@ -618,16 +618,17 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       nn += e[2];
     }
     const size_t c = (size_t)blockIdx.x * a.CoutW + n0 + col;
-    if (fwdstat)
+    if (fwdstat && a.fin.counter)
+      st_sc1_f4(a.stats + c * 4, make_float4(S1, S2, K, nn));   // handed to the last workgroup
+    else if (fwdstat)
       *reinterpret_cast<float4 *>(a.stats + c * 4) = make_float4(S1, S2, K, nn);
     else
       *reinterpret_cast<float2 *>(a.stats + c * 2) = make_float2(S1, S2);
   }
   if (fwdstat && a.fin.counter) {   // fused BatchNorm finalize (BnFin, common.h)
-    __syncthreads();
     if (bn_fin_ticket(a.fin.counter, reinterpret_cast<int *>(smem))) {
       bn_fwd_finalize_tail(a.stats, a.fin, reinterpret_cast<double *>(smem));
-      if (tid == 0) *a.fin.counter = 0u;
+      if (tid == 0) bn_fin_reset(a.fin.counter);
     }
   }
 #undef KA
@@ -738,7 +739,9 @@ __global__ void __launch_bounds__(256) bconv_reduce_kernel(const GConvArgs a, in
         tn += red[q][2];
       }
       const int c = tid * GV + k;
-      if (fwdstat)
+      if (fwdstat && a.fin.counter)
+        st_sc1_f4(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 4, make_float4(t1, t2, piv[k], tn));
+      else if (fwdstat)
         *reinterpret_cast<float4 *>(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 4) =
             make_float4(t1, t2, piv[k], tn);
       else
@@ -750,7 +753,7 @@ __global__ void __launch_bounds__(256) bconv_reduce_kernel(const GConvArgs a, in
     __shared__ int fflag;
     if (bn_fin_ticket(a.fin.counter, &fflag)) {
       bn_fwd_finalize_tail(a.stats, a.fin, fred);
-      if (tid == 0) *a.fin.counter = 0u;
+      if (tid == 0) bn_fin_reset(a.fin.counter);
     }
   }
 }

@@ -291,23 +291,45 @@ __device__ __forceinline__ void bn_fwd_finalize_tail(const float *stats, const B
   }
 }
 
-// Ticket of a workgroup that has written its statistics row; true for the last.
-// Writers publish with an agent-scope RELEASE fence only (L2 write-back, no
-// invalidate: a full __threadfence in every workgroup invalidates the XCD's
-// L2 under the still-running workgroups); the last one ACQUIREs.
+// Hand-off of the statistics rows to the last workgroup without an L2
+// write-back (cdna_hip_programming.md §6 Guideline 16, sc1 form): the rows are
+// stored write-through (agent-scope atomic 8-byte stores = sc1), every wave
+// drains its stores, then one lane takes a ticket (relaxed agent fetch_add);
+// the workgroup with the last ticket acquires (one lane) and reads the rows
+// with plain loads.  (A release fence per workgroup writes back its XCD's
+// whole L2 under the still-running workgroups: measured +35..60 us a layer.)
+typedef __attribute__((address_space(1))) unsigned long long hcu_gu64;
+typedef __attribute__((address_space(1))) unsigned hcu_gu32;
+__device__ __forceinline__ void st_sc1_f4(float *p, float4 v) {
+  const unsigned long long lo = ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
+  const unsigned long long hi = ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z);
+  __hip_atomic_store((hcu_gu64 *)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((hcu_gu64 *)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Ticket of a workgroup whose waves have stored their rows with st_sc1_f4;
+// true (after the acquire) for the last workgroup.  flag_lds: one int of LDS.
 __device__ __forceinline__ bool bn_fin_ticket(unsigned *counter, int *flag_lds) {
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-    *flag_lds = atomicAdd(counter, 1u) == nb - 1 ? 1 : 0;
+    const unsigned t = __hip_atomic_fetch_add((hcu_gu32 *)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = t == nb - 1 ? 1 : 0;
   }
   __syncthreads();
   const bool last = *(volatile int *)flag_lds != 0;
   __syncthreads();
-  if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (last) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
   return last;
+}
+__device__ __forceinline__ void bn_fin_reset(unsigned *counter) {
+  __hip_atomic_store((hcu_gu32 *)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
 // (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n
@@ -361,6 +383,7 @@ inline int plan_conv_fp32(GConvArgs &a, int target_blocks) {
   return plan_conv_any(a, target_blocks);
 }
 int launch_bconv(const GConvArgs &a, hipStream_t s);
+void bconv_tuning(bool on);   // measured planning on/off for the plans built by this thread
 int bconv_stat_rows(const GConvArgs &a);
 inline int launch_conv_any(const GConvArgs &a, hipStream_t s) {
   if (a.use_bconv) return launch_bconv(a, s);
@@ -650,7 +673,7 @@ struct PrepJob {
   // CONVT_DGRAD: Cin, Cout, T, UCs, CinW
   int p[16];
 };
-constexpr int kPrepBatch = 12;
+constexpr int kPrepBatch = 32;   // jobs per launch: the batch is a kernel argument (< 4 KB)
 int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n, hipStream_t s);
 
 // Loss / optimizer (loss_adam.hip)

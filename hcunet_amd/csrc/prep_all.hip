@@ -14,6 +14,7 @@ struct PrepBatch {
   int n;
   PrepJob j[kPrepBatch];
 };
+static_assert(sizeof(PrepBatch) <= 4000, "prep batch must fit the 4 KB kernel-argument limit");
 
 __device__ __forceinline__ bool prep_index2(const WPack &pk, uint32_t i, int T, int ICs, int CoutW,
                                             int &t, int &ci, int &co) {

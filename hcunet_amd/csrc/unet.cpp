@@ -919,7 +919,9 @@ int hcu_unet_plan_create_ex(const hcu_unet_spec *spec, int B, int X, int Y, int 
   p->X = X;
   p->Y = Y;
   p->Z = Z;
+  bconv_tuning((flags & HCU_PLAN_FORWARD_ONLY) == 0);
   const int e = build_plan(*p);
+  bconv_tuning(true);
   if (e) {
     delete p;
     *out = nullptr;
