@@ -238,6 +238,8 @@ def main():
     ap.add_argument('--config', default='2', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--fresh-input', action='store_true',
+                    help='clone the input every step (data-loader pattern; checks graph re-use)')
     ap.add_argument('--infer', action='store_true',
                     help='tiled inference driver throughput (SURVEY 8f-1) instead of training')
     args = ap.parse_args()
@@ -265,7 +267,8 @@ def main():
     def step():
         opt.zero_grad()
         with torch.autocast('cuda', dtype=torch.bfloat16, enabled=bf16):
-            out = model(x)
+            # --fresh-input: a new input tensor every step, as a data loader hands over
+            out = model(x.clone() if args.fresh_input else x)
             loss = cross_entropy(out, mask, pwl, method='pixel')
         loss.backward()
         hcunet_amd.dist.allreduce_gradients(model)

@@ -973,15 +973,16 @@ int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int 
 }
 
 static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,
-                           hipStream_t stream) {
+                           hipStream_t stream, bool input_done = false) {
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
   if (training) HCU_HIP(hipMemsetAsync(c.fptr(c.sc, p.fin_off), 0, 64, c.s));
   tag(std::string("in"), "fwd");
-  if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
-                           t->x_dtype))
-    return e;
+  if (!input_done)
+    if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
+                             t->x_dtype))
+      return e;
   tag(std::string("prep"), "fwd");
   if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_jobs.data(),
                               (int)p.prep_jobs.size(), c.s))
@@ -1071,12 +1072,20 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
         if (L.bn.count <= 1.0)
           return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
   }
-  std::vector<uintptr_t> key = {0, (uintptr_t)t->x, (uintptr_t)t->out, (uintptr_t)t->params,
-                                (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)training,
-                                (uintptr_t)t->x_dtype};
-  append_bn_key(key, p, t);
-  return run_graphed(p, key, (hipStream_t)stream,
-                     [&](hipStream_t s) { return enqueue_forward(p, t, training, s); });
+  // The input layout change runs ahead of the captured sequence, so a fresh
+  // input tensor every step (a data loader) does not key a new graph.
+  if (graphs_enabled() && !timing_on()) {
+    tag(std::string("in"), "fwd");
+    if (int e = launch_to_cl(t->x, reinterpret_cast<float *>((char *)t->saved + p.xcl_off), p.B, p.xin.C,
+                             p.xin.Cs, p.xin.vox() / p.B, (hipStream_t)stream, p.es == 2, t->x_dtype))
+      return e;
+    std::vector<uintptr_t> key = {0, (uintptr_t)t->out, (uintptr_t)t->params, (uintptr_t)t->saved,
+                                  (uintptr_t)t->scratch, (uintptr_t)training};
+    append_bn_key(key, p, t);
+    return run_graphed(p, key, (hipStream_t)stream,
+                       [&](hipStream_t s) { return enqueue_forward(p, t, training, s, true); });
+  }
+  return enqueue_forward(p, t, training, (hipStream_t)stream);
 }
 
 static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout,
@@ -1255,7 +1264,7 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
   const hcu_unet_plan &p = *plan;
   if (p.flags & HCU_PLAN_FORWARD_ONLY)
     return fail(HCU_ERR_INVALID, "backward through a forward-only plan (its activations are not kept)");
-  std::vector<uintptr_t> key = {1, (uintptr_t)t->x, (uintptr_t)t->params, (uintptr_t)t->grads,
+  std::vector<uintptr_t> key = {1, (uintptr_t)t->params, (uintptr_t)t->grads,
                                 (uintptr_t)t->saved, (uintptr_t)t->scratch, (uintptr_t)dout,
                                 (uintptr_t)dx, (uintptr_t)training, (uintptr_t)accumulate};
   // Per-launch timing attributes kernel time to layers: keep it serial.

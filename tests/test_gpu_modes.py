@@ -76,3 +76,35 @@ def test_fused_bn_finalize_matches_separate(tmp_path):
             assert torch.equal(b, c)
             tol = 1e-4 * max(a.abs().max().item(), 1e-6)
             assert (a - b).abs().max().item() <= tol
+
+
+def test_fresh_input_every_step_matches():
+    """A new input tensor each step (data-loader pattern: the input layout change
+    runs ahead of the captured graph) gives the same outputs and gradients as
+    re-using one tensor."""
+    from hcat.loss import cross_entropy
+    from hcat.unet import Unet_Constructor
+    from oracle import inputs
+    kw = dict(image_dimensions=3, in_channels=4, out_channels=1, feature_sizes=[4, 8, 16],
+              kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)}, upsample_kernel=(2, 2, 2),
+              max_pool_kernel=(2, 2, 1), upsample_stride=(2, 2, 1))
+    xs = [torch.from_numpy(inputs.make_x((2, 4, 44, 44, 6), seed=s)).cuda() for s in (1, 2, 3)]
+    res = []
+    for fresh in (False, True):
+        torch.manual_seed(0)
+        m = Unet_Constructor(**kw).cuda().train()
+        outs = []
+        for it in range(6):
+            for p in m.parameters():
+                p.grad = None
+            x = xs[it % 3].clone() if fresh else xs[it % 3]
+            out = m(x)
+            ms = (2, 1) + tuple(out.shape[2:])
+            loss = cross_entropy(out, torch.from_numpy(inputs.make_mask(ms)).cuda(),
+                                 torch.from_numpy(inputs.make_pwl(ms)).cuda(), method='pixel')
+            loss.backward()
+            outs.append([out.detach().cpu()] + [p.grad.detach().cpu() for p in m.parameters()])
+        res.append(outs)
+    for a_it, b_it in zip(*res):
+        for a, b in zip(a_it, b_it):
+            assert torch.equal(a, b)
