@@ -471,6 +471,8 @@ struct WGradFinalize {
   int accumulate;
 };
 int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s);
+constexpr int kWgfBatch = 24;   // finalize jobs per launch (kernel argument < 4 KB)
+int launch_wgrad_finalize_batch(const WGradFinalize *fs, int n, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Pointwise / reduction kernels (pointwise.hip)

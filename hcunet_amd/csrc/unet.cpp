@@ -343,6 +343,7 @@ struct hcu_unet_plan {
   size_t buf_off[HCU_NBUF] = {};
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
   size_t fin_off = 0;   // fused BatchNorm finalize ticket counter (zeroed per forward)
+  size_t wpart_floats = 0;   // weight-gradient slab arena (deferred, batched finalizes)
   size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
   // Captured launch sequences (hipGraph) keyed by the buffers they bake in:
   // forward and backward are fixed kernel sequences, so a replay costs one
@@ -614,7 +615,10 @@ int build_plan(hcu_unet_plan &p) {
   // scratch are backward-only
   for (size_t &b : p.buf_off) b = scratch.take_floats(fwd_only ? 0 : p.max_act);
   p.part_off = scratch.take_floats(p.max_part);
-  p.wpart_off = scratch.take_floats(fwd_only ? 0 : p.max_part);
+  // the slab arena holds several layers' weight-gradient partials until their
+  // finalizes run together (at least one layer's, at most 8 M floats beyond)
+  p.wpart_floats = fwd_only ? 0 : std::max<size_t>(p.max_part, (size_t)8 << 20);
+  p.wpart_off = scratch.take_floats(p.wpart_floats);
   p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
   p.fin_off = scratch.take_floats(16);
@@ -641,6 +645,37 @@ struct Ctx {
   int bf() const { return p.es == 2; }   // bf16 activation storage
   float *part() const { return fptr(sc, p.part_off); }
   float *wpart() const { return fptr(sc, split ? p.wpart_off : p.part_off); }
+  // Weight-gradient slab arena: each layer's partial slabs stay until its
+  // finalize runs; finalizes are deferred and launched together (one batched
+  // kernel on the branch stream) when the next slab would not fit, and at the
+  // end of the backward.  Nothing else reads or writes the arena.
+  size_t wp_off = 0;
+  std::vector<WGradFinalize> pend;
+  // HCU_WGF_DEFER=0: finalize each layer right after its weight gradient (A/B)
+  static bool defer_wgf() {
+    static const bool on = !(getenv("HCU_WGF_DEFER") && getenv("HCU_WGF_DEFER")[0] == '0');
+    return on;
+  }
+  int pend_wgf(const WGradFinalize &f) {
+    pend.push_back(f);
+    return defer_wgf() ? 0 : flush_wgf();
+  }
+  int flush_wgf() {
+    int e = 0;
+    if (!pend.empty()) e = launch_wgrad_finalize_batch(pend.data(), (int)pend.size(), wstream());
+    pend.clear();
+    wp_off = 0;
+    return e;
+  }
+  // Arena space for `floats` (flushing the deferred finalizes first if needed).
+  int slab(size_t floats, float *&ptr) {
+    const size_t need = (floats + 63) / 64 * 64;
+    if (wp_off + need > p.wpart_floats || pend.size() >= 64)
+      if (int e = flush_wgf()) return e;
+    ptr = fptr(sc, p.wpart_off) + wp_off;
+    wp_off += need;
+    return 0;
+  }
   float *wprep() const { return fptr(sc, p.wprep_off); }
   float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
   float *kpart() const { return fptr(sc, p.kpart_off); }
@@ -764,10 +799,10 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   w.a_scale = asc;
   w.a_shift = ash;
   w.G = dy;
-  w.partial = c.wpart();
+  if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
   if (int e = launch_wgrad(w, c.wstream())) return e;
   WGradFinalize f{};
-  f.partial = c.wpart();
+  f.partial = w.partial;
   f.dw = c.G + L.w_off;
   f.db = c.G + L.b_off;
   f.KB = w.KB;
@@ -781,7 +816,7 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   f.fold_mod = L.fold_mod;
   f.ACs = w.ACs;
   f.accumulate = accumulate;
-  if (int e = launch_wgrad_finalize(f, c.wstream())) return e;
+  if (int e = c.pend_wgf(f)) return e;   // finalized with the next flush (Ctx::slab / end of backward)
   if (int e = c.read_done(dy_slot)) return e;
   if (!dA) return 0;
   tag(L.name, "dgrad");
@@ -1149,9 +1184,11 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.fork()) return e;
     {
       const int R = chansum_rows(u.out.vox(), u.out.Cs);
-      if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, c.wpart(), R, c.wstream(), c.bf()))
+      float *cs = nullptr;
+      if (int e = c.slab((size_t)R * u.out.Cs, cs)) return e;
+      if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, cs, R, c.wstream(), c.bf()))
         return e;
-      if (int e = launch_reduce_partials(c.wpart(), R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate,
+      if (int e = launch_reduce_partials(cs, R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate,
                                          c.wstream()))
         return e;
     }
@@ -1161,10 +1198,10 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       w.a_scale = bp.scale;
       w.a_shift = bp.shift;
       w.G = dU;
-      w.partial = c.wpart();
+      if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
       if (int e = launch_wgrad(w, c.wstream())) return e;
       WGradFinalize f{};
-      f.partial = c.wpart();
+      f.partial = w.partial;
       f.dw = c.G + u.w_off;
       f.db = nullptr;
       f.KB = w.KB;
@@ -1176,7 +1213,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       f.CoutT = u.Cout;
       f.GCs = w.GCs;
       f.accumulate = accumulate;
-      if (int e = launch_wgrad_finalize(f, c.wstream())) return e;
+      if (int e = c.pend_wgf(f)) return e;
     }
     if (int e = c.read_done(su)) return e;
     tag(u.name, "dgrad");
@@ -1231,6 +1268,8 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
         return e;
     }
   }
+  tag(std::string("wgrad"), "finalize");
+  if (int e = c.flush_wgf()) return e;
   if (int e = c.join()) return e;
   if (timing_on()) timing_set_tag("");
   return HCU_OK;

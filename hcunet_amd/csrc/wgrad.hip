@@ -678,8 +678,26 @@ int launch_wgrad(const WGradArgs &a, hipStream_t s) {
 // both the elements and the slabs: S threads share one element (each sums the
 // slabs k = s, s+S, ... in fp64), then the S sums are combined in LDS in a
 // fixed order.  The result is scattered into the PyTorch weight layout.
+__device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int S, double *red);
 __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize f, int S) {
   __shared__ double red[256];
+  wgrad_finalize_body(f, S, red);
+}
+// Several layers' finalizes in one launch (grid.y = job): the backward defers
+// each layer's finalize until its slabs would no longer fit the slab arena.
+struct WGFBatch {
+  int n;
+  int S[kWgfBatch], blocks[kWgfBatch];
+  WGradFinalize f[kWgfBatch];
+};
+static_assert(sizeof(WGFBatch) <= 4000, "finalize batch must fit the 4 KB kernel-argument limit");
+__global__ void __launch_bounds__(256) wgrad_finalize_batch_kernel(const WGFBatch b) {
+  __shared__ double red[256];
+  const int j = blockIdx.y;
+  if ((int)blockIdx.x >= b.blocks[j]) return;
+  wgrad_finalize_body(b.f[j], b.S[j], red);
+}
+__device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int S, double *red) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
   const int EPB = 256 / S;
   const int tid = threadIdx.x, el = tid % EPB, sl = tid / EPB;
@@ -723,12 +741,37 @@ __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize
   }
 }
 
-int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s) {
+static void wgf_geometry(const WGradFinalize &f, int &S, int &blocks) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
-  int S = 1;
+  S = 1;
   while (S < 64 && S * 2 <= f.KB && n * S / 256 < 1024) S *= 2;
   const int EPB = 256 / S;
-  const int blocks = (int)((n + EPB - 1) / EPB);
+  blocks = (int)((n + EPB - 1) / EPB);
+}
+
+int launch_wgrad_finalize_batch(const WGradFinalize *fs, int n, hipStream_t s) {
+  for (int j0 = 0; j0 < n; j0 += kWgfBatch) {
+    WGFBatch b{};
+    b.n = std::min(kWgfBatch, n - j0);
+    int gx = 1;
+    double by = 0.0;
+    for (int k = 0; k < b.n; ++k) {
+      b.f[k] = fs[j0 + k];
+      wgf_geometry(b.f[k], b.S[k], b.blocks[k]);
+      gx = std::max(gx, b.blocks[k]);
+      by += 4.0 * (double)b.f[k].Mtot * b.f[k].Ntot * (b.f[k].KB + 1);
+    }
+    HCU_TIMED(s, "wgrad_finalize_batch_kernel", 0.0, by,
+              hipLaunchKernelGGL(wgrad_finalize_batch_kernel, dim3(gx, b.n), dim3(256), 0, s, b));
+    HCU_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s) {
+  const int64_t n = (int64_t)f.Mtot * f.Ntot;
+  int S, blocks;
+  wgf_geometry(f, S, blocks);
   HCU_TIMED(s, "wgrad_finalize_kernel", 0.0, 4.0 * (double)n * (f.KB + 1),
             hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f, S));
   HCU_CHECK_LAUNCH();
