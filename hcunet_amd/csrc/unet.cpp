@@ -775,15 +775,28 @@ bool fuse_bnbwd(const Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
 }
 
 // Finalize + apply of a BatchNorm backward whose reduction ran in a dgrad epilogue.
+// BatchNorm-backward finalize + apply: two launches; HCU_BNFA=1 fuses them
+// for layers with few partial rows (launch_bn_bwd_finalize_apply) -- measured
+// equal within noise on MI355X, so the simpler form stays the default.
+static int bn_fin_apply(const float *part, int R, int W, const BNLayer &bn, BNCoef coef, float *G,
+                        int training, int accumulate, float *dz, const float *y, int64_t nvox, int Cs,
+                        hipStream_t s, int bf) {
+  static const bool sep = !(getenv("HCU_BNFA") && getenv("HCU_BNFA")[0] == '1');
+  if (sep) {
+    if (int e = launch_bn_bwd_finalize(part, R, bn.C, bn.Cs, W, bn.count, coef, G + bn.gamma, G + bn.beta,
+                                       training, accumulate, s))
+      return e;
+    return launch_bn_bwd_apply(dz, y, coef, nvox, Cs, s, bf);
+  }
+  return launch_bn_bwd_finalize_apply(part, R, W, bn.C, bn.Cs, bn.count, coef, G + bn.gamma, G + bn.beta,
+                                      training, accumulate, dz, y, nvox, s, bf);
+}
+
 int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *dz, int training,
                  int accumulate) {
   const BNCoef coef = coef_at(c.sv, bnl.bn);
-  if (int e = launch_bn_bwd_finalize(c.part(), gconv_rows(a), bnl.bn.C, bnl.bn.Cs, a.CoutW,
-                                     bnl.bn.count, coef, c.G + bnl.bn.gamma, c.G + bnl.bn.beta,
-                                     training, accumulate, c.s))
-    return e;
-  return launch_bn_bwd_apply(dz, c.fptr(c.sv, bnl.y_off), coef, bnl.out.vox(), bnl.out.Cs, c.s,
-                             c.bf());
+  return bn_fin_apply(c.part(), gconv_rows(a), a.CoutW, bnl.bn, coef, c.G, training, accumulate, dz,
+                      c.fptr(c.sv, bnl.y_off), bnl.out.vox(), bnl.out.Cs, c.s, c.bf());
 }
 
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
@@ -854,10 +867,8 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
                                            c.bf()))
       return e;
   }
-  if (int e = launch_bn_bwd_finalize(c.part(), R, L.bn.C, L.bn.Cs, L.bn.Cs, L.bn.count, coef,
-                                     c.G + L.bn.gamma, c.G + L.bn.beta, training, accumulate, c.s))
-    return e;
-  return launch_bn_bwd_apply(dbuf, y, coef, nvox, L.out.Cs, c.s, c.bf());
+  return bn_fin_apply(c.part(), R, L.bn.Cs, L.bn, coef, c.G, training, accumulate, dbuf, y, nvox,
+                      L.out.Cs, c.s, c.bf());
 }
 
 }  // namespace
@@ -1149,12 +1160,8 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = launch_outconv_wfinalize(part_oc, R, p.Co, last.out.C, last.out.Cs, c.G + p.oc_w,
                                          c.G + p.oc_b, accumulate, c.s))
       return e;
-    if (int e = launch_bn_bwd_finalize(part_bn, R, last.bn.C, last.bn.Cs, last.bn.Cs, last.bn.count, coef,
-                                       c.G + last.bn.gamma, c.G + last.bn.beta, training,
-                                       accumulate, c.s))
-      return e;
-    if (int e = launch_bn_bwd_apply(c.buf(cur), c.fptr(c.sv, last.y_off), coef, nvox,
-                                    last.out.Cs, c.s, c.bf()))
+    if (int e = bn_fin_apply(part_bn, R, last.bn.Cs, last.bn, coef, c.G, training, accumulate,
+                             c.buf(cur), c.fptr(c.sv, last.y_off), nvox, last.out.Cs, c.s, c.bf()))
       return e;
   }
   // decoder, last to first
