@@ -465,7 +465,7 @@ struct WGradFinalize {
   const float *partial;
   float *dw, *db;
   int KB, Mtot, Ntot, T;
-  int mode;
+  int mode;   // 0 Conv3d (taps rows), 1 ConvTranspose3d, 2 bias column sums (db[c < Cout])
   int Cout, Cin_g, groups, fold_mod, ACs;   // conv
   int Cin, CoutT, GCs;                      // convT
   int accumulate;

@@ -1195,9 +1195,16 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.slab((size_t)R * u.out.Cs, cs)) return e;
       if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, cs, R, c.wstream(), c.bf()))
         return e;
-      if (int e = launch_reduce_partials(cs, R, u.out.Cs, u.Cout, c.G + u.b_off, accumulate,
-                                         c.wstream()))
-        return e;
+      WGradFinalize fb{};   // the bias: column sums of the R rows, with the batched finalizes
+      fb.partial = cs;
+      fb.db = c.G + u.b_off;
+      fb.KB = R;
+      fb.Mtot = 1;
+      fb.Ntot = u.out.Cs;
+      fb.mode = 2;
+      fb.Cout = u.Cout;
+      fb.accumulate = accumulate;
+      if (int e = c.pend_wgf(fb)) return e;
     }
     {
       WGradArgs w = u.wg;

@@ -715,6 +715,10 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
   for (int j = 1; j < S; ++j) s += red[j * EPB + el];
   const float v = (float)s;
   const int grow = (int)(idx / f.Ntot), gcol = (int)(idx % f.Ntot);
+  if (f.mode == 2) {   // column sums of R rows (ConvTranspose bias: rows = chansum partials)
+    if (gcol < f.Cout && f.db) f.db[gcol] = f.accumulate ? f.db[gcol] + v : v;
+    return;
+  }
   if (f.mode == 0) {
     const int o = gcol;
     if (o >= f.Cout) return;
