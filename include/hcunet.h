@@ -4,7 +4,9 @@
  * This library replaces the arithmetic behind the reference's Python operator
  * interface for ONE path: hcat.unet.Unet_Constructor forward + backward, the
  * pixel-weighted BCE loss (hcat.loss.cross_entropy, method='pixel') and the
- * Adam step that follows it in the reference training pattern.  The reference
+ * Adam step that follows it in the reference training pattern -- plus the
+ * callers either side of it: the tiled inference driver, the
+ * input transforms and the reference's other losses.  The reference
  * binds no native code (it calls stock torch.nn ops), so each entry point below
  * names the reference symbol whose semantics it implements; the Python host
  * layer (hcunet_amd/, re-exported as hcat.unet / hcat.loss) binds these through
@@ -13,7 +15,10 @@
  * Conventions
  *   - Every pointer is a device (HBM) pointer owned by the caller.  No entry
  *     point allocates device memory for tensors; scratch/saved workspaces are
- *     sized by the *_bytes / *_query functions and passed in.
+ *     sized by the *_bytes / *_query functions and passed in.  One exception:
+ *     creating a TRAINING plan times the best few convolution tilings on a
+ *     private, grown-on-demand device arena (hipMalloc, kept for the process;
+ *     HCU_BCONV_TUNE=0 disables the timing).
  *   - Work is enqueued asynchronously on `stream` (a hipStream_t, 0 = null
  *     stream).  The per-op launchers are stateless and re-entrant.
  *   - A network plan (hcu_unet_plan) is NOT read-only after creation: on first
