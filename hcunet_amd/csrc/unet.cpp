@@ -335,6 +335,9 @@ struct hcu_unet_plan {
   int64_t n_params = 0;
   int n_bn = 0;
   std::vector<PrepJob> prep_jobs;  // weight re-layouts, one batched launch per forward
+  // the same split: images the forward reads / input-gradient images only the
+  // backward reads (re-laid on the branch stream while the forward runs)
+  std::vector<PrepJob> prep_fwd, prep_bwd;
   size_t saved_bytes = 0, scratch_bytes = 0;
   // scratch layout
   // Backward gradient buffers: a ring of HCU_NBUF activation-sized slots, so
@@ -343,6 +346,7 @@ struct hcu_unet_plan {
   size_t buf_off[HCU_NBUF] = {};
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
   size_t fin_off = 0;   // fused BatchNorm finalize ticket counter (zeroed per forward)
+  double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
   size_t wpart_floats = 0;   // weight-gradient slab arena (deferred, batched finalizes)
   size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
   // Captured launch sequences (hipGraph) keyed by the buffers they bake in:
@@ -602,6 +606,10 @@ int build_plan(hcu_unet_plan &p) {
     const int pd[5] = {u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW};
     add_job(PREP_CONVT_DGRAD, prep_elems(u.dgrad), u.w_off, wpack_of(u.dgrad), pd, 5, u.wd_off);
   }
+  p.prep_fwd.clear();
+  p.prep_bwd.clear();
+  for (const PrepJob &j : p.prep_jobs)
+    (j.kind == PREP_CONV_DGRAD || j.kind == PREP_CONVT_DGRAD ? p.prep_bwd : p.prep_fwd).push_back(j);
   if (fwd_only) {
     size_t mx = 1;
     for (const auto &a : acts) mx = std::max(mx, a.second);
@@ -609,6 +617,11 @@ int build_plan(hcu_unet_plan &p) {
     for (size_t k = 0; k < acts.size(); ++k) *acts[k].first = pp[k & 1];
   }
   p.saved_bytes = saved.off;
+  // forward convolution FLOPs: decides graph replay vs direct launches
+  p.fwd_flops = 0.0;
+  for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
+    for (const ConvLayer &cl : *v)
+      p.fwd_flops += 2.0 * cl.fwd.B * cl.fwd.OX * cl.fwd.OY * cl.fwd.OZ * (double)cl.Cout * cl.Cin_g * cl.T;
 
   Region scratch;
   // the gradient ring, the weight-gradient partials and the weight re-layout
@@ -875,12 +888,23 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
 
 namespace {
 
-bool graphs_enabled() {   // HCU_GRAPHS=0 launches kernel by kernel (debugging, A/B)
-  static const bool on = [] {
+// hipGraph replay of the captured sequences vs direct launches.  On MI355X /
+// ROCm 7 a replayed kernel node costs ~1.5 us more on the GPU than a direct
+// launch (config 3: 7.24 vs 7.10 ms per step), but a direct launch costs the
+// host ~10 us: at config 2 (2.3 ms of GPU work, 1.7 ms of host enqueue) direct
+// launches ran 2.31..3.34 ms per step depending on host jitter, graphs a
+// steady 2.51..2.58.  So: graphs for plans whose forward is under 100 GFLOP,
+// direct launches above; HCU_GRAPHS=0 / 1 forces either (A/B, debugging).
+int graphs_forced() {
+  static const int v = [] {
     const char *e = getenv("HCU_GRAPHS");
-    return !(e && e[0] == '0');
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
-  return on;
+  return v;
+}
+bool graphs_for(const hcu_unet_plan &p) {
+  const int f = graphs_forced();
+  return f >= 0 ? f == 1 : p.fwd_flops < 100e9;
 }
 
 void append_bn_key(std::vector<uintptr_t> &key, const hcu_unet_plan &p, const hcu_unet_tensors *t) {
@@ -897,7 +921,7 @@ void append_bn_key(std::vector<uintptr_t> &key, const hcu_unet_plan &p, const hc
 // are off or per-launch timing is on.
 template <class F>
 int run_graphed(const hcu_unet_plan &p, std::vector<uintptr_t> key, hipStream_t s, F enqueue) {
-  if (!graphs_enabled() || timing_on()) return enqueue(s);
+  if (!graphs_for(p) || timing_on()) return enqueue(s);
   int dev = 0;
   HCU_HIP(hipGetDevice(&dev));
   key.push_back((uintptr_t)dev);
@@ -1018,9 +1042,14 @@ int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int 
   return p->n_bn;
 }
 
+int ensure_side(const hcu_unet_plan &p, int dev);
+bool side_enabled();
+
 static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,
-                           hipStream_t stream, bool input_done = false) {
+                           hipStream_t stream, bool input_done = false, bool split = false) {
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  c.split = split;
+  c.ws = split ? p.side : c.s;
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
   if (training) HCU_HIP(hipMemsetAsync(c.fptr(c.sc, p.fin_off), 0, 64, c.s));
@@ -1030,8 +1059,14 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
                              t->x_dtype))
       return e;
   tag(std::string("prep"), "fwd");
-  if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_jobs.data(),
-                              (int)p.prep_jobs.size(), c.s))
+  if (training && !p.prep_bwd.empty()) {   // eval forwards never need the dgrad images
+    if (int e = c.fork()) return e;
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
+                                (int)p.prep_bwd.size(), c.wstream()))
+      return e;
+  }
+  if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data(),
+                              (int)p.prep_fwd.size(), c.s))
     return e;
   const float *src = xcl;
   const float *ssc = nullptr, *ssh = nullptr;
@@ -1100,6 +1135,7 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
     return e;
   if (training && t->bn_num_batches_tracked)
     if (int e = launch_bn_count_increment(t->bn_num_batches_tracked, p.n_bn, c.s)) return e;
+  if (int e = c.join()) return e;
   if (timing_on()) timing_set_tag("");
   return HCU_OK;
 }
@@ -1120,18 +1156,30 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   }
   // The input layout change runs ahead of the captured sequence, so a fresh
   // input tensor every step (a data loader) does not key a new graph.
-  if (graphs_enabled() && !timing_on()) {
+  // training forwards re-lay the input-gradient weight images on the branch
+  // stream (forked / joined inside the forward); one user of it at a time
+  static const bool fwd_side = !(getenv("HCU_FWD_SIDE") && getenv("HCU_FWD_SIDE")[0] == '0');   // A/B
+  const bool split = fwd_side && training && side_enabled() && !timing_on() &&
+                     !(p.flags & HCU_PLAN_FORWARD_ONLY);
+  std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
+  if (split) {
+    lk.lock();
+    int dev = 0;
+    HCU_HIP(hipGetDevice(&dev));
+    if (int e = ensure_side(p, dev)) return e;
+  }
+  if (graphs_for(p) && !timing_on()) {
     tag(std::string("in"), "fwd");
     if (int e = launch_to_cl(t->x, reinterpret_cast<float *>((char *)t->saved + p.xcl_off), p.B, p.xin.C,
                              p.xin.Cs, p.xin.vox() / p.B, (hipStream_t)stream, p.es == 2, t->x_dtype))
       return e;
     std::vector<uintptr_t> key = {0, (uintptr_t)t->out, (uintptr_t)t->params, (uintptr_t)t->saved,
-                                  (uintptr_t)t->scratch, (uintptr_t)training};
+                                  (uintptr_t)t->scratch, (uintptr_t)training, (uintptr_t)split};
     append_bn_key(key, p, t);
     return run_graphed(p, key, (hipStream_t)stream,
-                       [&](hipStream_t s) { return enqueue_forward(p, t, training, s, true); });
+                       [&](hipStream_t s) { return enqueue_forward(p, t, training, s, true, split); });
   }
-  return enqueue_forward(p, t, training, (hipStream_t)stream);
+  return enqueue_forward(p, t, training, (hipStream_t)stream, false, split);
 }
 
 static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout,

@@ -3,8 +3,8 @@
 HCU_SIDE (weight-gradient branch on its own stream) and HCU_GRAPHS (hipGraph
 capture/replay) are read once per process, so each mode runs in a child
 process started before any GPU call of its own: one with both off (serial,
-kernel-by-kernel on one stream), one with the defaults (graphs + split
-streams).  A missing event wait on the gradient-slot ring would make the
+kernel-by-kernel on one stream), one with graphs + split streams and one
+with the default (split streams, direct launches).  A missing event wait on the gradient-slot ring would make the
 split run read a slot the chain has already rewritten, which shows up as a
 bitwise difference in the gradients."""
 import os
@@ -59,9 +59,11 @@ def _run(tmp_path, tag, env_extra):
 def test_split_graphed_equals_serial(tmp_path):
     serial = _run(tmp_path, 'serial', {'HCU_SIDE': '0', 'HCU_GRAPHS': '0'})
     split = _run(tmp_path, 'split', {'HCU_SIDE': '1', 'HCU_GRAPHS': '1'})
+    direct = _run(tmp_path, 'direct', {'HCU_SIDE': '1', 'HCU_GRAPHS': '0'})   # the default
     for it in range(3):
-        for a, b in zip(serial[it], split[it]):
+        for a, b, d in zip(serial[it], split[it], direct[it]):
             assert torch.equal(a, b)
+            assert torch.equal(a, d)
 
 
 def test_fused_bn_finalize_matches_separate(tmp_path):
