@@ -893,8 +893,8 @@ namespace {
 // launch (config 3: 7.24 vs 7.10 ms per step), but a direct launch costs the
 // host ~10 us: at config 2 (2.3 ms of GPU work, 1.7 ms of host enqueue) direct
 // launches ran 2.31..3.34 ms per step depending on host jitter, graphs a
-// steady 2.51..2.58.  So: graphs for plans whose forward is under 100 GFLOP,
-// direct launches above; HCU_GRAPHS=0 / 1 forces either (A/B, debugging).
+// steady 2.51..2.58.  So: graphs for the forward of plans under 100 GFLOP,
+// direct launches otherwise; HCU_GRAPHS=0 / 1 forces either everywhere.
 int graphs_forced() {
   static const int v = [] {
     const char *e = getenv("HCU_GRAPHS");
@@ -902,9 +902,14 @@ int graphs_forced() {
   }();
   return v;
 }
-bool graphs_for(const hcu_unet_plan &p) {
+// The backward (two streams joined by events) replays slower still: a graph
+// of it cost 0.17 ms per config-2 step against direct launches (forward-only
+// graph 2.39 ms/step vs both graphed 2.56, three interleaved A/B runs), so by
+// default only a small plan's forward is replayed.
+bool graphs_for(const hcu_unet_plan &p, bool backward) {
   const int f = graphs_forced();
-  return f >= 0 ? f == 1 : p.fwd_flops < 100e9;
+  if (f >= 0) return f == 1;
+  return !backward && p.fwd_flops < 100e9;
 }
 
 void append_bn_key(std::vector<uintptr_t> &key, const hcu_unet_plan &p, const hcu_unet_tensors *t) {
@@ -921,7 +926,7 @@ void append_bn_key(std::vector<uintptr_t> &key, const hcu_unet_plan &p, const hc
 // are off or per-launch timing is on.
 template <class F>
 int run_graphed(const hcu_unet_plan &p, std::vector<uintptr_t> key, hipStream_t s, F enqueue) {
-  if (!graphs_for(p) || timing_on()) return enqueue(s);
+  if (!graphs_for(p, key[0] != 0) || timing_on()) return enqueue(s);
   int dev = 0;
   HCU_HIP(hipGetDevice(&dev));
   key.push_back((uintptr_t)dev);
@@ -1168,7 +1173,7 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
     HCU_HIP(hipGetDevice(&dev));
     if (int e = ensure_side(p, dev)) return e;
   }
-  if (graphs_for(p) && !timing_on()) {
+  if (graphs_for(p, false) && !timing_on()) {
     tag(std::string("in"), "fwd");
     if (int e = launch_to_cl(t->x, reinterpret_cast<float *>((char *)t->saved + p.xcl_off), p.B, p.xin.C,
                              p.xin.Cs, p.xin.vox() / p.B, (hipStream_t)stream, p.es == 2, t->x_dtype))
