@@ -95,16 +95,16 @@ __device__ __forceinline__ void ldc(const float *p, float (&f)[N]) {   // fp32 c
 // here in fp64, in a fixed order, by the parallel-variance identity:
 //   mean = sum_r (S1_r + n_r K_r) / N
 //   M2   = sum_r (S2_r - S1_r^2 / n_r) + sum_r n_r (K_r + S1_r / n_r - mean)^2
+// Sum over the 256 threads: an xor butterfly of wave shuffles (IEEE addition
+// is commutative, so both partners hold the same bits), then the 4 wave sums
+// in a fixed order -- 2 barriers instead of a 9-barrier LDS tree.
 __device__ double block_sum_f64(double v, double *red) {
-  const int tid = threadIdx.x;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   __syncthreads();
-  red[tid] = v;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) red[tid] += red[tid + off];
-    __syncthreads();
-  }
-  return red[0];
+  return ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 __global__ void __launch_bounds__(256)
@@ -194,17 +194,19 @@ bn_bwd_finalize_kernel(const float *part, int R, int C, int W, double count,
       s2 += (double)part[((size_t)r * W + c) * 2 + 1];
     }
   }
-  r1[tid] = s1;
-  r2[tid] = s2;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) {
-      r1[tid] += r1[tid + off];
-      r2[tid] += r2[tid + off];
-    }
-    __syncthreads();
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
   }
+  if ((tid & 63) == 0) {
+    r1[tid >> 6] = s1;
+    r2[tid >> 6] = s2;
+  }
+  __syncthreads();
   if (tid != 0) return;
+  r1[0] = ((r1[0] + r1[1]) + r1[2]) + r1[3];
+  r2[0] = ((r2[0] + r2[1]) + r2[2]) + r2[3];
   if (c >= C) {
     coef.c1[c] = coef.c0[c] = 0.f;
     return;
