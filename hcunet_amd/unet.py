@@ -375,6 +375,8 @@ class _Engine:
         # collective (hcunet_amd.dist.allreduce_gradients).
         self.comm_flat = None
         self.params = None
+        self._slots = None   # (module, name) of each parameter, in self.params order
+        self._bns = None
         self._bn_arrays = None
 
     def check_input(self, x, bf16=False):
@@ -406,10 +408,28 @@ class _Engine:
     def params_ready(self, require_gpu=True):
         """Ensure every parameter is a view of one flat fp32 buffer (a device
         buffer for the native path; require_gpu=False lays out host tensors the
-        same way, for the CPU tests of the data-parallel host logic)."""
+        same way, for the CPU tests of the data-parallel host logic).  The
+        per-step check follows the (module, name) slots recorded at layout
+        time: a replaced Parameter or moved storage is detected; a whole
+        submodule swapped into the network after the first forward is not
+        (rebuild the model, as the reference's own load() does)."""
         m = self.module_ref
-        params = list(m.parameters())
         flat = self.flat
+        ok = flat is not None and self.params is not None and self._slots is not None
+        if ok:
+            # fast path: the (module, name) slots recorded at layout time still
+            # hold the same Parameter objects, each still a view of the flat
+            # buffer (no recursive module walk per step: host time)
+            base = flat.data_ptr()
+            off = 0
+            for (mod, name), q in zip(self._slots, self.params):
+                if mod._parameters.get(name) is not q or q.data_ptr() != base + 4 * off:
+                    ok = False
+                    break
+                off += q.numel()
+        if ok:
+            return self.params
+        params = list(m.parameters())
         ok = flat is not None and self.params is not None and len(params) == len(self.params)
         if ok:
             base = flat.data_ptr()
@@ -419,6 +439,12 @@ class _Engine:
                     ok = False
                     break
                 off += p.numel()
+        if ok:
+            self._slots = [(mod, name) for _, mod in m.named_modules()
+                           for name, prm in mod._parameters.items() if prm is not None]
+            if len(self._slots) != len(params) or any(mod._parameters[n] is not q
+                                                      for (mod, n), q in zip(self._slots, params)):
+                self._slots = None
         if not ok:
             dev = params[0].device
             for p in params:
@@ -442,11 +468,17 @@ class _Engine:
             self.grad_flat = None
             self.comm_flat = None
             self._bn_arrays = None
+            self._slots = [(mod, name) for _, mod in m.named_modules()
+                           for name, prm in mod._parameters.items() if prm is not None]
+            if len(self._slots) != len(params) or any(mod._parameters[n] is not q
+                                                      for (mod, n), q in zip(self._slots, params)):
+                self._slots = None   # unusual registration order: keep the full check
         return self.params
 
     def bn_arrays(self):
         if self._bn_arrays is None:
             bns = bn_modules(self.module_ref)
+            self._bns = bns
             for bn in bns:
                 if bn.running_mean.dtype != torch.float32 or not bn.running_mean.is_contiguous():
                     raise RuntimeError('hcunet_amd: BatchNorm running stats must be contiguous fp32')
@@ -456,7 +488,7 @@ class _Engine:
             nb = (ctypes.c_void_p * n)(*[bn.num_batches_tracked.data_ptr() for bn in bns])
             self._bn_arrays = (rm, rv, nb, [bn.running_mean.data_ptr() for bn in bns])
         else:
-            bns = bn_modules(self.module_ref)
+            bns = self._bns
             if [bn.running_mean.data_ptr() for bn in bns] != self._bn_arrays[3]:
                 self._bn_arrays = None
                 return self.bn_arrays()
