@@ -33,6 +33,9 @@ from hcat.loss import cross_entropy  # noqa: E402
 from hcat.unet import Unet_Constructor  # noqa: E402
 import hcunet_amd  # noqa: E402
 from hcunet_amd import _lib  # noqa: E402
+from hcunet_amd import roofline as roofline_mod  # noqa: E402
+
+PROFILE_TAG = 'r03'   # the round whose committed profiles/ summaries bench.py cites
 
 METRIC = "training voxels/sec (fwd+bwd+step), 5-level 3D U-Net, 256×256×16×4 tiles"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, dense
@@ -124,9 +127,10 @@ def tagify(rocprof_name):
 
 def load_traffic(kernel, config='2'):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/traffic.json, written by tools/pmc_traffic.py), or None."""
+    (profiles/<PROFILE_TAG>_traffic_config<config>.json, written by
+    tools/pmc_traffic.py), or None."""
     tab = None
-    for fn in ('traffic_config%s.json' % config, 'traffic.json' if config == '2' else None):
+    for fn in ('%s_traffic_config%s.json' % (PROFILE_TAG, config),):
         if not fn:
             continue
         try:
@@ -145,12 +149,64 @@ def load_traffic(kernel, config='2'):
     return tot / n if n else None
 
 
+def layer_of(key):
+    """'kernel@d0.c1.fwd' -> ('d0.c1', 'fwd'); pool -> ('d0.pool', 'fwd');
+    untagged / bookkeeping launches -> their own groups."""
+    kern, _, tag = key.partition('@')
+    if kern.startswith('wgrad_finalize'):
+        return 'wgrad.finalize', 'bwd'
+    if not tag:
+        base = kern.split('<')[0].replace('_kernel', '')
+        return {'loss_pixel': 'loss', 'loss_finalize': 'loss', 'scale': 'loss',
+                'adam': 'adam'}.get(base, base), '-'
+    parts = tag.split('.')
+    if len(parts) >= 3:
+        layer, phase = '.'.join(parts[:2]), '.'.join(parts[2:])
+        if phase == 'pool':
+            return parts[0] + '.pool', 'fwd'
+        return layer, phase
+    return parts[0], '.'.join(parts[1:]) or '-'
+
+
+def layer_table(detail, cfg, B, steps):
+    """Per-layer roofline fractions: each layer's algorithmic FLOPs and
+    compulsory bytes (hcunet_amd/roofline.py), its roofline time
+    max(bytes / HBM peak, FLOPs / MFMA peak) and the kernel time measured for
+    it (HIP events around every launch tagged with the layer, serialized
+    pass), per step."""
+    bf16 = cfg['dtype'] == 'bf16'
+    ref = {r['layer']: r for r in roofline_mod.layers(cfg['kw'], B, TILE, bf16)}
+    rows = {}
+    for k, v in detail.items():
+        layer, phase = layer_of(k)
+        r = rows.setdefault(layer, dict(layer=layer, us=0.0, launches=0.0, kernels={}))
+        us = v['ms'] * 1e3 / steps
+        r['us'] += us
+        r['launches'] += v['count'] / steps
+        kk = '%s:%s' % (phase, k.partition('@')[0])
+        r['kernels'][kk] = round(r['kernels'].get(kk, 0.0) + us, 2)
+    out = []
+    for layer, r in rows.items():
+        a = ref.get(layer)
+        row = dict(layer=layer, measured_us=round(r['us'], 2), launches=r['launches'],
+                   kernels=r['kernels'])
+        if a:
+            row.update(gflop=a['flops'] / 1e9, compulsory_mb=a['bytes'] / 1e6,
+                       roof_us=round(a['roof_us'], 2), frac=a['roof_us'] / r['us'] if r['us'] else None,
+                       bound='mfma' if a['flops'] / (roofline_mod.PEAK_BF16 if bf16 else roofline_mod.PEAK_FP32)
+                       > a['bytes'] / roofline_mod.PEAK_HBM else 'hbm')
+        out.append(row)
+    order = [r['layer'] for r in roofline_mod.layers(cfg['kw'], B, TILE, bf16)]
+    out.sort(key=lambda r: (order.index(r['layer']) if r['layer'] in order else len(order), r['layer']))
+    return out
+
+
 def rocprof_avg_us(kernel, config):
     """Average duration (us) of `kernel` in the committed rocprofv3
     --kernel-trace --stats summary of this config's graphed bench step
-    (profiles/r02_kernel_stats_config<config>.csv), or None."""
+    (profiles/<PROFILE_TAG>_kernel_stats_config<config>.csv), or None."""
     import csv
-    path = os.path.join(ROOT, 'profiles', 'r02_kernel_stats_config%s.csv' % config)
+    path = os.path.join(ROOT, 'profiles', '%s_kernel_stats_config%s.csv' % (PROFILE_TAG, config))
     try:
         with open(path, newline='') as f:
             rows = list(csv.DictReader(f))
@@ -300,13 +356,26 @@ def main():
 
     roofline = None
     kernels = None
+    layer_rows = None
+    tiling = dict(zip(('table_entries', 'timed_by_this_process'), _lib.tuning_entries()))
+    tiling['mode'] = _lib.tuning_mode()
+    if os.environ.get('HCU_TUNE_SAVE'):
+        tiling['saved'] = _lib.tuning_save(os.environ['HCU_TUNE_SAVE'])
     if not args.no_kernel_timing:
         _lib.lib().hcu_timing_enable(args.steps * 512)
+        _lib.lib().hcu_timing_detail(1)
         for _ in range(args.steps):
             step()
         sync()
-        rep = _lib.timing_report()
+        detail = _lib.timing_report()
+        _lib.lib().hcu_timing_detail(0)
         _lib.lib().hcu_timing_disable()
+        layer_rows = layer_table(detail, cfg, B, args.steps)
+        rep = {}
+        for k, v in detail.items():   # per kernel symbol
+            r = rep.setdefault(k.partition('@')[0], dict(count=0, ms=0.0, flops=0.0, bytes=0.0))
+            for f in r:
+                r[f] += v[f]
         total_ms = sum(v['ms'] for v in rep.values())
         name, d = max(rep.items(), key=lambda kv: kv[1]['ms'])
         avg_s = d['ms'] / d['count'] / 1e3
@@ -318,10 +387,15 @@ def main():
         else:
             ach = d['bytes'] / d['count'] / avg_s / 1e9
             bound, peak, unit = 'hbm', PEAK_HBM_GBS, 'GB/s'
+        rp_us = rocprof_avg_us(name, args.config)
+        per_launch = (d['flops'] if d['flops'] > 0 else d['bytes']) / d['count']
         roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit,
                     "frac": ach / peak, "traffic": load_traffic(name, args.config), "kernel": name,
                     "avg_launch_us": avg_s * 1e6,
-                    "rocprof_avg_launch_us": rocprof_avg_us(name, args.config),
+                    "rocprof_avg_launch_us": rp_us,
+                    # the same fraction from the committed rocprofv3 summary's average
+                    "frac_rocprof": (per_launch / (rp_us * 1e-6) / (1e12 if d['flops'] > 0 else 1e9) / peak
+                                     if rp_us else None),
                     "launches_per_step": d['count'] / args.steps,
                     "flops_per_launch": d['flops'] / d['count'],
                     "share_of_kernel_time": d['ms'] / total_ms}
@@ -348,13 +422,17 @@ def main():
                            "global_batch": B * world, "per_gpu_batch": B,
                            "parallelism": "dp%d" % world, "final_loss": final_loss,
                            "host_enqueue_ms_per_step": t_enq / args.steps * 1e3},
-                "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
-        if cfg.get('roof_ms'):
-            # SURVEY §8d per-layer roofline of the whole step (sum over layers of
-            # max(bytes / 8 TB/s, flops / dense MFMA peak)) vs the measured step
-            line["step_roofline"] = {"per_layer_roofline_ms": cfg['roof_ms'],
-                                     "measured_ms": ms_per_step,
-                                     "frac": cfg['roof_ms'] / ms_per_step}
+                "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
+                "tiling": tiling}
+        # SURVEY §8d per-layer roofline of the whole step (sum over layers of
+        # max(bytes / 8 TB/s, flops / dense MFMA peak), hcunet_amd/roofline.py)
+        # vs the measured step
+        roof_ms, roof_fl, roof_by = roofline_mod.step_roofline(cfg['kw'], B, TILE, bf16)
+        line["step_roofline"] = {"per_layer_roofline_ms": roof_ms, "measured_ms": ms_per_step,
+                                 "frac": roof_ms / ms_per_step, "flops": roof_fl,
+                                 "compulsory_bytes": roof_by}
+        if layer_rows is not None:
+            line["layers"] = layer_rows
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

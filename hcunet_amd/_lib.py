@@ -123,7 +123,37 @@ SYMBOLS = [
     ("hcu_timing_disable", _I, []),
     ("hcu_timing_detail", _I, [_I]),
     ("hcu_timing_report", _I64, [ctypes.c_char_p, _I64]),
+    ("hcu_tuning_set_mode", _I, [_I]),
+    ("hcu_tuning_get_mode", _I, []),
+    ("hcu_tuning_entries", _I64, [ctypes.POINTER(_I64)]),
+    ("hcu_tuning_save", _I64, [ctypes.c_char_p]),
 ]
+
+TUNE_MODEL, TUNE_TABLE, TUNE_TIMED = 0, 1, 2
+
+
+def tuning_mode(mode=None):
+    """Get (mode=None) or set the convolution tiling mode (include/hcunet.h):
+    0 cost model, 1 persistent table + cost model on a miss (deterministic
+    across processes), 2 table + timing on a miss (default)."""
+    L = lib()
+    if mode is not None:
+        check(L.hcu_tuning_set_mode(int(mode)), 'hcu_tuning_set_mode')
+    return int(L.hcu_tuning_get_mode())
+
+
+def tuning_entries():
+    """(entries in the tiling table, entries timed by this process)."""
+    timed = ctypes.c_int64()
+    n = lib().hcu_tuning_entries(ctypes.byref(timed))
+    return int(n), int(timed.value)
+
+
+def tuning_save(path=None):
+    n = lib().hcu_tuning_save(path.encode() if path else None)
+    if n < 0:
+        raise RuntimeError(last_error())
+    return int(n)
 
 _lib = None
 

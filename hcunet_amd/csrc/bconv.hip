@@ -3,6 +3,10 @@
 // instances are in bconv_f32.hip (separate translation unit: compile time).
 #include "bconv_kernel.h"
 
+#include <dlfcn.h>
+
+#include <cstdio>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
@@ -56,13 +60,67 @@ int bconv_stat_rows(const GConvArgs &a) {
 static void bconv_finish(GConvArgs &a, int ntz, int VEC, int fpf);
 
 // ---- measured planning: times a candidate on scratch buffers of its shapes
+//
+// Choices are kept per convolution signature as the tiling itself
+// (CK, NSUB, MPW), in memory and in a persistent table (tuning/bconv_gfx950.txt
+// next to libhcunet.so, or HCU_TUNE_FILE) loaded on first use, so every
+// process -- every data-parallel rank -- plans the same tiling for the same
+// convolution, and timing dispatches never run inside a measured step.
+// Modes (hcu_tuning_set_mode / HCU_BCONV_TUNE): 0 = the cost model's first
+// choice; 1 = the table, the cost model on a miss (deterministic across
+// processes: what a data-parallel job uses); 2 = the table, timing on a miss
+// (default).
 static std::mutex g_tune_mu;
-static std::map<std::string, int> g_tune;
+static std::map<std::string, std::string> g_tune;   // signature -> "CK,NSUB,MPW"
+static bool g_tune_loaded = false;
+static int g_tune_mode = -1;
+static long g_tune_timed = 0;   // signatures timed by this process
 // Measured planning is off while a forward-only (inference) plan is built: its
 // tile-batch size follows the free device memory, so every call can bring new
 // signatures, and timing those costs seconds per call.
 static thread_local bool g_tune_off = false;
 void bconv_tuning(bool on) { g_tune_off = !on; }
+
+static std::string tune_file() {
+  if (const char *e = getenv("HCU_TUNE_FILE")) return e;
+  Dl_info info;
+  if (dladdr(reinterpret_cast<void *>(&bconv_tuning), &info) && info.dli_fname) {
+    std::string p = info.dli_fname;
+    const size_t slash = p.rfind('/');
+    return (slash == std::string::npos ? std::string(".") : p.substr(0, slash)) +
+           "/tuning/bconv_gfx950.txt";
+  }
+  return "";
+}
+
+// Loads the persistent table once (caller holds g_tune_mu).
+static void tune_load_locked() {
+  if (g_tune_loaded) return;
+  g_tune_loaded = true;
+  if (g_tune_mode < 0) {
+    const char *e = getenv("HCU_BCONV_TUNE");
+    g_tune_mode = e ? std::max(0, std::min(2, atoi(e))) : 2;
+  }
+  const std::string path = tune_file();
+  if (path.empty()) return;
+  FILE *f = fopen(path.c_str(), "r");
+  if (!f) return;
+  char line[1024];
+  while (fgets(line, sizeof line, f)) {
+    if (line[0] == '#') continue;
+    char *bar = strchr(line, '|');
+    if (!bar) continue;
+    *bar = 0;
+    std::string val = bar + 1;
+    while (!val.empty() && (val.back() == '\n' || val.back() == '\r' || val.back() == ' ')) val.pop_back();
+    g_tune[line] = val;
+  }
+  fclose(f);
+}
+
+static std::string tiling_key(const GConvArgs &c) {
+  return std::to_string(c.CK) + "," + std::to_string(c.NSUB) + "," + std::to_string(c.MPW);
+}
 
 static std::string bconv_signature(const GConvArgs &a) {
   const int v[] = {a.bes, a.B, a.IX, a.IY, a.IZ, a.ICs, a.OX, a.OY, a.OZ, a.SX, a.SY, a.SZ, a.OCs,
@@ -257,19 +315,27 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
                    [](const Cand &x, const Cand &y) { return x.cost < y.cost; });
   for (Cand &cd : cands) bconv_finish(cd.c, ntz, VEC, fpf);
   a = cands[0].c;
-  // Measured choice among the model's best candidates (HCU_BCONV_TUNE=0: the
-  // model's first choice), remembered per convolution signature.
+  // Measured choice among the model's best candidates, remembered per
+  // convolution signature (table above).
   const int top = std::min<int>((int)cands.size(), env_int_b("HCU_BCONV_TUNE_TOP", 6));
-  // Not for very large convolutions (~10^8 output voxels: seconds of timing)
-  // nor in forward-only plans (g_tune_off).
-  const double out_vox = (double)a.B * a.OX * a.OY * a.OZ;
-  if (env_int_b("HCU_BCONV_TUNE", 1) && top > 1 && !fck && !fns && !fmp && out_vox <= 16e6 && !g_tune_off) {
+  if (!fck && !fns && !fmp) {
     const std::string key = bconv_signature(a);
     std::lock_guard<std::mutex> lk(g_tune_mu);
-    auto it = g_tune.find(key);
+    tune_load_locked();
+    auto it = g_tune_mode > 0 ? g_tune.find(key) : g_tune.end();
+    bool hit = false;
     if (it != g_tune.end()) {
-      a = cands[std::min<int>(it->second, (int)cands.size() - 1)].c;
-    } else {
+      for (const Cand &cd : cands)
+        if (tiling_key(cd.c) == it->second) {
+          a = cd.c;
+          hit = true;
+          break;
+        }
+    }
+    // Time on a miss -- not for very large convolutions (~10^8 output voxels:
+    // seconds of timing) nor in forward-only plans (g_tune_off).
+    const double out_vox = (double)a.B * a.OX * a.OY * a.OZ;
+    if (!hit && g_tune_mode == 2 && top > 1 && out_vox <= 16e6 && !g_tune_off) {
       double best_us = 1e300;
       int best_i = 0;
       bool timed = false;
@@ -282,7 +348,10 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
           best_i = i;
         }
       }
-      if (timed) g_tune[key] = best_i;
+      if (timed) {
+        g_tune[key] = tiling_key(cands[best_i].c);
+        ++g_tune_timed;
+      }
       a = cands[best_i].c;
     }
   }
@@ -343,3 +412,46 @@ int launch_bconv(const GConvArgs &a, hipStream_t s) {
 }
 
 }  // namespace hcu
+
+extern "C" {
+
+int hcu_tuning_set_mode(int mode) {
+  if (mode < 0 || mode > 2) return hcu::fail(1, "tuning mode must be 0, 1 or 2");
+  std::lock_guard<std::mutex> lk(hcu::g_tune_mu);
+  hcu::tune_load_locked();
+  hcu::g_tune_mode = mode;
+  return 0;
+}
+
+int hcu_tuning_get_mode(void) {
+  std::lock_guard<std::mutex> lk(hcu::g_tune_mu);
+  hcu::tune_load_locked();
+  return hcu::g_tune_mode;
+}
+
+// Entries in the table (loaded + timed by this process); *timed (nullable)
+// receives the number this process timed.
+int64_t hcu_tuning_entries(int64_t *timed) {
+  std::lock_guard<std::mutex> lk(hcu::g_tune_mu);
+  hcu::tune_load_locked();
+  if (timed) *timed = hcu::g_tune_timed;
+  return (int64_t)hcu::g_tune.size();
+}
+
+// Writes the whole table (sorted by signature) to `path` (null: the table the
+// library loads); returns the number of entries or -1.
+int64_t hcu_tuning_save(const char *path) {
+  std::lock_guard<std::mutex> lk(hcu::g_tune_mu);
+  hcu::tune_load_locked();
+  const std::string p = path ? std::string(path) : hcu::tune_file();
+  FILE *f = p.empty() ? nullptr : fopen(p.c_str(), "w");
+  if (!f) return -hcu::fail(1, "cannot write tuning table " + p);
+  fprintf(f, "# bconv tiling per convolution signature (bes,B,IX,IY,IZ,ICs,OX,OY,OZ,SX,SY,SZ,OCs,Cout,"
+             "osx,osy,osz,ofx,ofy,ofz,KX,KY,KZ,sx,sy,sz,dx,dy,dz,px,py,pz,nph,phx,phy,phz | CK,NSUB,MPW),\n"
+             "# measured on MI355X by plan-time timing (hcunet_amd/csrc/bconv.hip)\n");
+  for (const auto &kv : hcu::g_tune) fprintf(f, "%s|%s\n", kv.first.c_str(), kv.second.c_str());
+  fclose(f);
+  return (int64_t)hcu::g_tune.size();
+}
+
+}  // extern "C"

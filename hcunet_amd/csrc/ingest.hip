@@ -6,9 +6,9 @@
 //   reshape     hcat/transforms.py:139-157  [Z,Y,X,C] -> [X,Y,Z,C]
 //   normalize   hcat/transforms.py:257-283  (v + -mean_c) / std_c (float64)
 //   to_tensor   hcat/transforms.py:118-137  float64 -> fp16, -> [1,C,X,Y,Z]
-// computes it: the arithmetic is float64 and the fp16 rounding is one
-// round-to-nearest-even of the float64 value (as torch.as_tensor does), so the
-// output is bit-identical.  The Z <-> X transpose goes through an LDS tile
+// computes it: the arithmetic is float64 and the fp16 rounding is torch's
+// (float64 -> float32 -> fp16, each to nearest even), so the output is
+// bit-identical.  The Z <-> X transpose goes through an LDS tile
 // (32 x by 32 z at one y): reads are contiguous along X*C, writes along Z.
 #include "common.h"
 #include "timing.h"
@@ -63,7 +63,10 @@ ingest_kernel(const T *src, int Z, int Y, int X, int C, int nzt, const IngestNor
       const size_t off = ((((size_t)b * Z + z0 + zi) * Y + y) * X + x0 + xi) * C + c;
       double v = (double)src[off] * nm.scale;   // exact: power-of-two scale
       if (nm.on) v = (v + -nm.mean[c]) / nm.std[c];
-      tile[(c * 32 + xi) * 33 + zi] = d2h_rne(v);
+      // torch.as_tensor(float64, dtype=half) rounds twice: float64 -> float32,
+      // then float32 -> fp16 (both to nearest even); a direct float64 -> fp16
+      // rounding differs where the float32 value lands on an fp16 midpoint.
+      tile[(c * 32 + xi) * 33 + zi] = d2h_rne((double)(float)v);
     }
   }
   __syncthreads();

@@ -9,6 +9,8 @@ averaged in the same collective so that every rank holds the same model (and a
 checkpoint saved by rank 0 is the job's model).  num_batches_tracked is equal
 on every rank by construction and is not reduced.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -85,10 +87,21 @@ def allreduce_gradients(module, group=None, bn_stats=True):
         off += k
 
 
+def deterministic_tiling():
+    """Every rank must run the same convolution tilings (the same summation
+    order): plan from the persistent tiling table, the cost model on a miss,
+    never from per-process timing (include/hcunet.h, hcu_tuning_set_mode)."""
+    from . import _lib
+    if os.path.exists(_lib.LIB_PATH) and _lib.tuning_mode() == _lib.TUNE_TIMED:
+        _lib.tuning_mode(_lib.TUNE_TABLE)
+
+
 def broadcast_parameters(module, src=0, group=None):
-    """Make every rank start from rank `src`'s parameters and BN buffers."""
+    """Make every rank start from rank `src`'s parameters and BN buffers (and
+    plan deterministic tilings, see deterministic_tiling)."""
     if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
+    deterministic_tiling()
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src=src, group=group)

@@ -321,6 +321,23 @@ int hcu_timing_detail(int on);
  * over launches; flops/bytes are algorithmic).  Returns bytes needed. */
 int64_t hcu_timing_report(char *buf, int64_t len);
 
+/* ------------------------------------------------------------------------ */
+/* Convolution tiling table.  Plans pick each convolution's tiling from a    */
+/* persistent table (tuning/bconv_gfx950.txt next to the library, or         */
+/* $HCU_TUNE_FILE) keyed by the convolution's signature, so every process    */
+/* and every data-parallel rank runs the same kernels (same summation order). */
+/* mode 0: cost model only; 1: table, cost model on a miss (deterministic    */
+/* across processes -- hcunet_amd.dist selects it); 2: table, the best few   */
+/* candidates timed on a miss (default; $HCU_BCONV_TUNE sets the initial     */
+/* mode).                                                                    */
+/* ------------------------------------------------------------------------ */
+int hcu_tuning_set_mode(int mode);
+int hcu_tuning_get_mode(void);
+/* Table entries; *timed (nullable) = entries timed by this process. */
+int64_t hcu_tuning_entries(int64_t *timed);
+/* Writes the table to path (NULL: the library's table file); entries or <0. */
+int64_t hcu_tuning_save(const char *path);
+
 #ifdef __cplusplus
 }
 #endif

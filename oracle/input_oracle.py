@@ -4,7 +4,7 @@ for one volume, the parity oracle of hcunet_amd.ingest (tests only).
   to_float   hcat/transforms.py:94-116   uint16 / 2**16, uint8 / 2**8 in float64
   reshape    hcat/transforms.py:139-157  [Z,Y,X,C] -> [X,Y,Z,C] (swapaxes(ndim-2, 0))
   normalize  hcat/transforms.py:257-283  per channel (v + -mean) / std, float64
-  to_tensor  hcat/transforms.py:118-137  float64 -> fp16, [X,Y,Z,C] -> [1,C,X,Y,Z]
+  to_tensor  hcat/transforms.py:118-137  float64 -> float32 -> fp16, [X,Y,Z,C] -> [1,C,X,Y,Z]
 
 Pinned against the reference's own transforms by tests/golden/input_path.npz
 (tests/golden/make_input_golden.py).
@@ -35,8 +35,11 @@ def normalize(a, mean, std):
 
 
 def to_tensor(a):
-    """float64 [X,Y,Z,C] -> fp16 [1,C,X,Y,Z] (one rounding, as torch.as_tensor)."""
-    return np.ascontiguousarray(np.moveaxis(a.astype(np.float16), -1, 0))[None]
+    """float64 [X,Y,Z,C] -> fp16 [1,C,X,Y,Z].  torch.as_tensor(float64, dtype=half)
+    (hcat/transforms.py:133) rounds float64 -> float32 -> fp16, each to nearest
+    even: so does this (a direct float64 -> fp16 rounding differs where the
+    float32 value lands on an fp16 midpoint)."""
+    return np.ascontiguousarray(np.moveaxis(a.astype(np.float32).astype(np.float16), -1, 0))[None]
 
 
 def network_input(raw, mean=None, std=None):

@@ -51,8 +51,10 @@ def test_stack_matches_reference(tmp_path):
         np.testing.assert_array_equal(bits(p), GOLD['stack.pwl'])
 
 
-def test_fp16_rounding_matches_numpy():
-    # float64 -> fp16 round-to-nearest-even over ties, subnormals, overflow, NaN/Inf
+def test_fp16_rounding_matches_torch():
+    # float64 -> fp16 as torch.as_tensor(float64, dtype=half) rounds (the
+    # reference's to_tensor, hcat/transforms.py:133): float64 -> float32 -> fp16,
+    # each to nearest even, over ties, near-ties, subnormals, overflow, NaN/Inf
     rng = np.random.default_rng(0)
     h = np.arange(0, 1 << 16, dtype=np.uint32).astype(np.uint16).view(np.float16)
     h = h[np.isfinite(h)].astype(np.float64)
@@ -61,13 +63,18 @@ def test_fp16_rounding_matches_numpy():
     vals = np.concatenate([h, mid, np.nextafter(mid, 0), np.nextafter(mid, np.inf),
                            rng.standard_normal(100000) * 10.0 ** rng.integers(-9, 6, 100000),
                            [65504.0, 65519.99, 65520.0, 1e6, -1e6, 2.0 ** -25, 2.0 ** -25 * 1.0000001,
-                            2.0 ** -26, 0.0, -0.0, np.inf, -np.inf, np.nan]])
+                            2.0 ** -26, 0.0, -0.0, np.inf, -np.inf, np.nan,
+                            1 + 3 * 2.0 ** -11 - 2.0 ** -30, -(1 + 3 * 2.0 ** -11 - 2.0 ** -30)]])
     vals = vals[np.isfinite(vals) | np.isinf(vals) | np.isnan(vals)]
     n = vals.size
     a = vals.reshape(1, 1, n, 1)                        # [Z=1, Y=1, X=n, C=1] float64
     v = ht.to_tensor()(a)                               # no to_float / reshape: [1,1,1,1,n]
     got = bits(v).reshape(-1)
-    want = vals.astype(np.float16).view(np.uint16)
+    want = torch.as_tensor(vals, dtype=torch.half).numpy().view(np.uint16)
+    # the float32 double-rounding case (just below an odd-mantissa fp16 midpoint)
+    # is among the values and differs from a direct float64 -> fp16 rounding
+    assert (np.float16(1 + 3 * 2.0 ** -11 - 2.0 ** -30).view(np.uint16)
+            != torch.as_tensor([1 + 3 * 2.0 ** -11 - 2.0 ** -30], dtype=torch.half).numpy().view(np.uint16)[0])
     nan = np.isnan(vals)
     np.testing.assert_array_equal(got[~nan], want[~nan])
     assert np.all((got[nan] & 0x7c00) == 0x7c00) and np.all((got[nan] & 0x3ff) != 0)

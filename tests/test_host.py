@@ -165,3 +165,33 @@ def test_inputs_generator_is_deterministic_and_in_range():
     assert set(m.reshape(-1).tolist()) <= {0.0, 1.0} and 0.4 < m.mean() < 0.6
     w = inputs.make_pwl((1, 1, 64, 64, 4))
     assert w.dtype.name == 'float16' and w.min() >= 0 and w.max() <= 11
+
+
+def test_step_roofline_matches_survey():
+    # config 2 50.17 GFLOP, 0.351 ms; config 3 1498.4 GFLOP, 0.891 ms
+    import bench
+    from hcunet_amd import roofline
+    ms, fl, by = roofline.step_roofline(bench.CONFIGS['2']['kw'], 2, (256, 256, 16))
+    assert abs(fl - 50.17e9) < 0.01e9 and abs(ms - 0.351) < 1e-3 and abs(by - 1.34e9) < 0.01e9
+    ms, fl, by = roofline.step_roofline(bench.CONFIGS['3']['kw'], 4, (256, 256, 16), bf16=True)
+    assert abs(fl - 1498.4e9) < 0.1e9 and abs(ms - 0.891) < 1e-3
+
+
+def test_tiling_table_modes_and_file(tmp_path):
+    # the persistent tiling table ships with the library and its modes switch
+    from hcunet_amd import _lib
+    table = os.path.join(os.path.dirname(_lib.LIB_PATH), 'tuning', 'bconv_gfx950.txt')
+    rows = [ln for ln in open(table) if not ln.startswith('#')]
+    assert len(rows) > 10 and all('|' in ln for ln in rows)
+    old = _lib.tuning_mode()
+    try:
+        assert _lib.tuning_mode(_lib.TUNE_TABLE) == _lib.TUNE_TABLE
+        n, timed = _lib.tuning_entries()
+        assert n >= len(rows) and timed == 0
+        out = tmp_path / 't.txt'
+        assert _lib.tuning_save(str(out)) == n
+        assert sorted(ln for ln in open(out) if not ln.startswith('#')) == sorted(rows)
+        with pytest.raises(ValueError):
+            _lib.tuning_mode(3)
+    finally:
+        _lib.tuning_mode(old)

@@ -49,3 +49,19 @@ def test_lazy_chain_records_steps_and_shapes():
 def test_stack_errors_like_reference(tmp_path):
     with pytest.raises(FileExistsError):
         Stack(str(tmp_path), [], [])
+
+
+def test_oracle_to_tensor_rounds_like_torch():
+    # torch.as_tensor(float64, dtype=half) (hcat/transforms.py:133) rounds
+    # float64 -> float32 -> fp16; values just below an odd-mantissa fp16
+    # midpoint expose a direct float64 -> fp16 rounding
+    import torch
+    v = 1 + 3 * 2.0 ** -11 - 2.0 ** -30
+    rng = np.random.default_rng(11)
+    # normalize-like values: (u / 2**16 + -mean) / std with non-trivial mean/std
+    u = rng.integers(0, 65536, 200000).astype(np.float64)
+    vals = np.concatenate([[v, -v], (u / 2 ** 16 + -0.37) / 0.213])
+    got = io.to_tensor(vals.reshape(-1, 1)).reshape(-1).view(np.uint16)
+    want = torch.as_tensor(vals, dtype=torch.half).numpy().view(np.uint16)
+    np.testing.assert_array_equal(got, want)
+    assert np.float16(v).view(np.uint16) != got[0]
