@@ -297,13 +297,270 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Pipelined form of bwgrad_kernel (same blocks, tiles, MFMA sequence and slab
+// layout, so the same sums in the same order): each thread keeps its share of
+// the NEXT tile's A halo and G image in registers -- NP 16-byte loads each,
+// issued right after the current tile is committed to LDS -- so the loads are
+// in flight while the current tile's MFMAs run, and a tile costs two LDS-only
+// barriers.  The halo coordinates of every register slot are tile-independent
+// and decoded once.
+template <int MSW, int NS, int NP>
+__global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  const int T = a.KX * a.KY * a.KZ;
+  const int CKA = a.CKA, CKG = a.CKG, RSA = a.PA2, RSG = a.PG2;
+  int tapc, cic, coc;
+  if (a.taps_rows) {
+    tapc = blockIdx.y / a.nci;
+    cic = blockIdx.y % a.nci;
+    coc = blockIdx.z;
+  } else {
+    cic = blockIdx.y;
+    tapc = blockIdx.z / a.nco;
+    coc = blockIdx.z % a.nco;
+  }
+  const int ci0 = cic * CKA, co0 = coc * CKG;
+  const int t0 = tapc * (a.taps_rows ? a.TA : a.TG);
+  const bool bias_block = a.taps_rows && a.bias_row && tapc == 0 && cic == 0;
+  const int HAV = a.HAV, HGV = a.HGV, PT = a.PTV;
+  uint16_t *alds = reinterpret_cast<uint16_t *>(smem);          // [HAV][RSA]
+  uint16_t *glds = alds + (size_t)HAV * RSA;                    // [HGV][RSG]
+  int *hvA = reinterpret_cast<int *>(glds + (size_t)HGV * RSG);  // [PT] A row * RSA
+  int *hvG = hvA + PT;                                           // [PT] G row * RSG
+  const int HAZ = a.HAZ, HAYZ = a.HAY * a.HAZ, HGZ = a.HGZ, HGYZ = a.HGY * a.HGZ;
+
+  for (int p = tid; p < PT; p += 256) {
+    int q, lz, lx, ly;
+    a.fTZ.divmod(p, q, lz);
+    a.fTY.divmod(q, lx, ly);
+    hvA[p] = (lx * a.asx * HAYZ + ly * a.asy * HAZ + lz * a.asz) * RSA;
+    hvG[p] = (lx * a.gsx * HGYZ + ly * a.gsy * HGZ + lz * a.gsz) * RSG;
+  }
+  const int rows_blk = a.taps_rows ? a.TA * CKA : CKA;
+  const int cols_blk = a.taps_rows ? CKG : a.TG * CKG;
+  int colA[MSW], colG[NS];
+#pragma unroll
+  for (int m = 0; m < MSW; ++m) {
+    const int r = (wave + 4 * m) * 16 + 4 * p4;
+    int off = 0;
+    if (r < rows_blk) {
+      if (a.taps_rows) {
+        const int ta = t0 + r / CKA, c = r % CKA;
+        if (ta < T) {
+          const int kz = ta % a.KZ, qq = ta / a.KZ, ky = qq % a.KY, kx = qq / a.KY;
+          off = (kx * a.adx * HAYZ + ky * a.ady * HAZ + kz * a.adz) * RSA + c;
+        }
+      } else {
+        off = r;
+      }
+    }
+    colA[m] = off;
+  }
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+    const int c = n * 16 + 4 * p4;
+    int off = 0;
+    if (c < cols_blk) {
+      if (a.taps_rows) {
+        off = c;
+      } else {
+        const int tg = t0 + c / CKG, o = c % CKG;
+        if (tg < T) {
+          const int kz = tg % a.KZ, qq = tg / a.KZ, ky = qq % a.KY, kx = qq / a.KY;
+          off = (kx * a.gdx * HGYZ + ky * a.gdy * HGZ + kz * a.gdz) * RSG + o;
+        }
+      }
+    }
+    colG[n] = off;
+  }
+
+  floatx4 acc[MSW][NS], accb[NS];
+#pragma unroll
+  for (int m = 0; m < MSW; ++m)
+#pragma unroll
+    for (int n = 0; n < NS; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int n = 0; n < NS; ++n) accb[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = bias_block && wave == 0;
+  const shortx8 ones = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};
+
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int CA8 = CKA / 8, CG8 = CKG / 8;
+  const bool act = a.a_scale != nullptr;
+  const int ca = tid % CA8, cg = tid % CG8;
+  const int va0 = tid / CA8, vsA = 256 / CA8, vg0 = tid / CG8, vsG = 256 / CG8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = act ? a.a_scale[ci0 + ca * 8 + k] : 1.f;
+    sh[k] = act ? a.a_shift[ci0 + ca * 8 + k] : 0.f;
+  }
+  // halo coordinates of each register slot: hx << 20 | hy << 10 | hz, -1 unused
+  int hoA[NP], hoG[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int v = va0 + k * vsA;
+    int q, hz, hx, hy;
+    a.fHAZ.divmod(v, q, hz);
+    a.fHAY.divmod(q, hx, hy);
+    hoA[k] = v < HAV ? (hx << 20) | (hy << 10) | hz : -1;
+    const int w = vg0 + k * vsG;
+    a.fHGZ.divmod(w, q, hz);
+    a.fHGY.divmod(q, hx, hy);
+    hoG[k] = w < HGV ? (hx << 20) | (hy << 10) | hz : -1;
+  }
+  const uint16_t *Ab = reinterpret_cast<const uint16_t *>(a.A);
+  const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
+  uint4 ra[NP], rg[NP];
+  unsigned oka = 0;
+
+  auto load = [&](int tt) {
+    const int b = tt / ntiles;
+    int tile = tt - b * ntiles;
+    const int tzi = tile % a.ntz;
+    tile /= a.ntz;
+    const int tyi = tile % a.nty, txi = tile / a.nty;
+    const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    {
+      const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
+      const uint16_t *base = Ab + (size_t)b * a.AX * a.AY * a.AZ * a.ACs + ci0 + ca * 8;
+      oka = 0;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int h = hoA[k];
+        const int gx = gx0 + (h >> 20), gy = gy0 + ((h >> 10) & 1023), gz = gz0 + (h & 1023);
+        const bool ok = h >= 0 && (unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY &&
+                        (unsigned)gz < (unsigned)a.AZ;
+        ra[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (ok) ra[k] = *reinterpret_cast<const uint4 *>(base + (((size_t)gx * a.AY + gy) * a.AZ + gz) * a.ACs);
+        oka |= (ok ? 1u : 0u) << k;
+      }
+    }
+    {
+      const int gx0 = px0 * a.gsx - a.gpx, gy0 = py0 * a.gsy - a.gpy, gz0 = pz0 * a.gsz - a.gpz;
+      const uint16_t *base = Gb + (size_t)b * a.GX * a.GY * a.GZ * a.GCs + co0 + cg * 8;
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        const int h = hoG[k];
+        const int gx = gx0 + (h >> 20), gy = gy0 + ((h >> 10) & 1023), gz = gz0 + (h & 1023);
+        // taps_rows: G is the output grid [PX][PY][PZ] (voxels past it are 0)
+        const bool ok = h >= 0 && (unsigned)gx < (unsigned)a.GX && (unsigned)gy < (unsigned)a.GY &&
+                        (unsigned)gz < (unsigned)a.GZ &&
+                        (!a.taps_rows || (gx < a.PX && gy < a.PY && gz < a.PZ));
+        rg[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (ok) rg[k] = *reinterpret_cast<const uint4 *>(base + (((size_t)gx * a.GY + gy) * a.GZ + gz) * a.GCs);
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      if (hoA[k] < 0) continue;
+      uint4 w = ra[k];
+      if (act && ((oka >> k) & 1u)) {
+        float f[8];
+        unpack8(w, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
+        w = pack8(f);
+      }
+      *reinterpret_cast<uint4 *>(alds + (size_t)(va0 + k * vsA) * RSA + ca * 8) = w;
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k)
+      if (hoG[k] >= 0) *reinterpret_cast<uint4 *>(glds + (size_t)(vg0 + k * vsG) * RSG + cg * 8) = rg[k];
+  };
+
+  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_beg = blockIdx.x * tpb_;
+  const int t_end = min(total, t_beg + tpb_);
+  if (t_beg < t_end) load(t_beg);
+  for (int tt = t_beg; tt < t_end; ++tt) {
+    lds_barrier();   // the previous tile's fragment reads are done
+    commit();
+    if (tt + 1 < t_end) load(tt + 1);   // in flight during this tile's MFMAs
+    lds_barrier();
+    for (int p0 = 0; p0 < PT; p0 += 32) {
+      const int pr = p0 + 8 * g + q4;
+      const int ra0 = hvA[pr], ra1 = hvA[pr + 4];
+      const int rg0 = hvG[pr], rg1 = hvG[pr + 4];
+      shortx8 bf[NS];
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        const shortx4 lo = tr_read(glds + rg0 + colG[n]);
+        const shortx4 hi = tr_read(glds + rg1 + colG[n]);
+        bf[n] = shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int m = 0; m < MSW; ++m) {
+        const shortx4 lo = tr_read(alds + ra0 + colA[m]);
+        const shortx4 hi = tr_read(alds + ra1 + colA[m]);
+        const shortx8 af = shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int n = 0; n < NS; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[n], acc[m][n], 0, 0, 0);
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int n = 0; n < NS; ++n)
+          accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bf[n], accb[n], 0, 0, 0);
+      }
+    }
+  }
+
+  const size_t slab = (size_t)blockIdx.x * a.Mtot;
+#pragma unroll
+  for (int m = 0; m < MSW; ++m) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = (wave + 4 * m) * 16 + g * 4 + r;
+      int grow = -1;
+      if (lr < rows_blk) {
+        if (a.taps_rows) {
+          const int ta = t0 + lr / CKA, ci = ci0 + lr % CKA;
+          if (ta < T && ci < a.ACs) grow = ta * a.ACs + ci;
+        } else if (ci0 + lr < a.ACs) {
+          grow = ci0 + lr;
+        }
+      }
+      if (grow < 0) continue;
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        const int lc = n * 16 + (lane & 15);
+        int gcol = -1;
+        if (lc < cols_blk) {
+          if (a.taps_rows) {
+            if (co0 + lc < a.GCs) gcol = co0 + lc;
+          } else {
+            const int tg = t0 + lc / CKG, o = co0 + lc % CKG;
+            if (tg < T && o < a.GCs) gcol = tg * a.GCs + o;
+          }
+        }
+        if (gcol >= 0) a.partial[(slab + grow) * a.Ntot + gcol] = acc[m][n][r];
+      }
+    }
+  }
+  if (do_bias && g == 0) {
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      const int lc = n * 16 + (lane & 15);
+      if (lc < CKG && co0 + lc < a.GCs)
+        a.partial[(slab + (size_t)T * a.ACs) * a.Ntot + co0 + lc] = accb[n][0];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 int plan_bwgrad(WGradArgs &a, int target_blocks) {
   a.use_bw = 0;
   const int T = a.KX * a.KY * a.KZ;
   if (a.ACs % 8 || a.GCs % 8) return fail(4, "bwgrad: channel strides must be multiples of 8");
   if (a.PX <= 0 || a.PY <= 0 || a.PZ <= 0) return fail(2, "bwgrad: empty grid");
-  if (a.apx || a.apy || a.apz || a.gpx || a.gpy || a.gpz)
-    return fail(4, "bwgrad: padded operands are not supported");
+  // padded operands (zero padding of A, or a cropped ConvTranspose3d output
+  // as G) are staged as zeros outside their grids
   // channel chunks: A side up to 32 channels, G side up to 64 (16-col subtiles)
   a.CKA = std::min(a.ACs, 32);
   if (a.ACs % a.CKA) a.CKA = 8;
@@ -380,7 +637,17 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   const long total = (long)a.B * a.ntx * a.nty * a.ntz;
   const long per = (long)a.mchunks * a.nchunks;
   a.occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
-  long kb = std::max(1L, (long)256 * a.occ / per);
+  // register prefetch slots per thread (pipelined kernel): max over threads of
+  // the 16-byte A / G loads one tile needs
+  const int nA = cdiv(a.HAV, 256 / (a.CKA / 8)), nG = cdiv(a.HGV, 256 / (a.CKG / 8));
+  const int np = std::max(nA, nG);
+  a.NPA = a.NPG = np <= 8 ? 8 : np <= 16 ? 16 : np <= 32 ? 32 : 0;
+  if (getenv("HCU_BWGRAD_SERIAL")) a.NPA = a.NPG = 0;   // A/B: the serial kernel
+  // One fp32 slab per block: the pipelined kernel hides its loads behind the
+  // MFMAs of the same block, so it needs at most two blocks per CU -- fewer
+  // blocks, fewer slabs for the finalize to read.
+  const int occ_kb = a.NPA ? std::min(a.occ, 2) : a.occ;
+  long kb = std::max(1L, (long)256 * occ_kb / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
   a.use_bw = 1;
@@ -404,15 +671,26 @@ int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
   const double by = 2.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
                            (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
   bool ok = false;
+#define BWP(MS_, NS_, NP_)                                                                  \
+  if (!ok && a.NPA == NP_) {                                                                \
+    HCU_TIMED(s, "bwgrad_pipe_kernel<" #MS_ "," #NS_ "," #NP_ ">", fl, by,                    \
+              hipLaunchKernelGGL((bwgrad_pipe_kernel<MS_, NS_, NP_>), grid, dim3(256),         \
+                                 a.lds_bytes, s, a));                                       \
+    ok = true;                                                                              \
+  }
 #define BW(MS_, NS_)                                                                        \
   if (!ok && a.MSW == MS_ && a.NSB <= NS_) {                                                \
-    HCU_TIMED(s, "bwgrad_kernel<" #MS_ "," #NS_ ">", fl, by,                                  \
-              hipLaunchKernelGGL((bwgrad_kernel<MS_, NS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    BWP(MS_, NS_, 8) BWP(MS_, NS_, 16) BWP(MS_, NS_, 32)                                    \
+    if (!ok) {                                                                              \
+      HCU_TIMED(s, "bwgrad_kernel<" #MS_ "," #NS_ ">", fl, by,                              \
+                hipLaunchKernelGGL((bwgrad_kernel<MS_, NS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    }                                                                                       \
     ok = true;                                                                              \
   }
   BW(1, 1) BW(1, 2) BW(1, 4) BW(1, 8) BW(3, 1) BW(3, 2) BW(3, 4) BW(5, 1) BW(5, 2) BW(5, 4)
   BW(9, 1) BW(9, 2) BW(9, 4)
 #undef BW
+#undef BWP
   if (!ok) return fail(4, "bwgrad: unsupported variant");
   HCU_CHECK_LAUNCH();
   return 0;

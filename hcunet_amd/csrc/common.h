@@ -440,6 +440,8 @@ struct WGradArgs {
   // are the LDS row strides of the A halo / G images, MSW the row subtiles per
   // wave, NSB the column subtiles of a block.
   int use_bw, MSW, NSB, PTV, HAV, HGV;
+  int NPA, NPG;                       // bwgrad: 16-byte A / G staging loads per thread and tile
+                                      // (register prefetch of the next tile); 0 = serial kernel
   // wgrad8 (wgrad8.hip, v2 == 2): A image z-row stride (PA2 / PG2: plane
   // strides), MFMA form (0: 16x16x4, 1: 4x4x1 16-block), voxel blocks per
   // instruction and z taps on the column side (form 1)
