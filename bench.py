@@ -286,6 +286,127 @@ def infer_main(args):
     print(json.dumps(line), flush=True)
 
 
+RUNET_TILE = (512, 512, 24)
+
+
+def runet_main(args):
+    """BASELINE config 5 on one GPU: hcat.r_unet.RDCNet(4, 5) (the model the
+    reference trains, tests/r_unet_test.py:19-56) on 512x512x24 tiles, B=1,
+    bf16 autocast, loss = cross_entropy(out[:, :1], pixel) + MSELoss(out[:, 2:])
+    then Adam; the input tiles come from pinned host memory, copied to the GPU
+    on a side stream while the previous step computes (a ring of two device
+    buffers).  One step = one tile."""
+    import hcat.loss as hl
+    from hcat.r_unet import RDCNet
+    device = torch.device('cuda', 0)
+    torch.manual_seed(0)
+    model = RDCNet(4, 5).to(device).train()
+    opt = hcunet_amd.optim.Adam(model.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(11)
+    n_host = 4
+    host = [((torch.randint(0, 65536, (1, 4) + RUNET_TILE, generator=g).float() / 65536 - 0.5) / 0.5)
+            .pin_memory() for _ in range(n_host)]
+    mask = (torch.rand((1, 1) + RUNET_TILE, generator=g) < 0.5).half().to(device)
+    pwl = (torch.rand((1, 1) + RUNET_TILE, generator=g) * 11.0).half().to(device)
+    vec = (torch.rand((1, 3) + RUNET_TILE, generator=g) * 2 - 1).to(device)
+    dev_buf = [torch.empty((1, 4) + RUNET_TILE, device=device) for _ in range(2)]
+    copy_stream = torch.cuda.Stream(device)
+    ready = [torch.cuda.Event() for _ in range(2)]
+    freed = [torch.cuda.Event() for _ in range(2)]
+    state = {'i': 0}
+
+    def prefetch(i):
+        slot = i % 2
+        with torch.cuda.stream(copy_stream):
+            copy_stream.wait_event(freed[slot])
+            dev_buf[slot].copy_(host[i % n_host], non_blocking=True)
+            ready[slot].record(copy_stream)
+
+    for s in range(2):
+        freed[s].record(torch.cuda.current_stream(device))
+    prefetch(0)
+
+    def step():
+        i = state['i']
+        slot = i % 2
+        prefetch(i + 1)                                   # next tile in flight during this step
+        torch.cuda.current_stream(device).wait_event(ready[slot])
+        opt.zero_grad()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = model(dev_buf[slot])
+            loss = hl.cross_entropy(out[:, 0:1], mask, pwl, method='pixel') + hl.MSELoss(out[:, 2:], vec)
+        freed[slot].record(torch.cuda.current_stream(device))
+        loss.backward()
+        opt.step()
+        state['i'] = i + 1
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize(device)
+    el = (time.perf_counter() - t0) / args.steps
+    vox = RUNET_TILE[0] * RUNET_TILE[1] * RUNET_TILE[2]
+    roofline = kernels = None
+    if not args.no_kernel_timing:
+        _lib.lib().hcu_timing_enable(args.steps * 2048)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(device)
+        rep = _lib.timing_report()
+        _lib.lib().hcu_timing_disable()
+        total_ms = sum(v['ms'] for v in rep.values())
+        name, d = max(rep.items(), key=lambda kv: kv[1]['ms'])
+        avg_s = d['ms'] / d['count'] / 1e3
+        bf_kernel = 'bf16' in name or name.startswith('bwgrad')
+        if d['flops'] > 0:
+            ach, bound, unit = d['flops'] / d['count'] / avg_s / 1e12, 'mfma', 'TFLOP/s'
+            peak = PEAK_BF16_MFMA_TFLOPS if bf_kernel else PEAK_FP32_MFMA_TFLOPS
+        else:
+            ach, bound, unit, peak = d['bytes'] / d['count'] / avg_s / 1e9, 'hbm', 'GB/s', PEAK_HBM_GBS
+        roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
+                    "traffic": None, "kernel": name, "avg_launch_us": avg_s * 1e6,
+                    "launches_per_step": d['count'] / args.steps, "share_of_kernel_time": d['ms'] / total_ms}
+        kernels = {"kernel_ms_per_step": total_ms / args.steps,
+                   "algorithmic_tflops_per_step": sum(v['flops'] for v in rep.values()) / args.steps / 1e12,
+                   "top": sorted(({"kernel": k, "ms_per_step": v['ms'] / args.steps,
+                                   "launches_per_step": v['count'] / args.steps} for k, v in rep.items()),
+                                 key=lambda r: -r['ms_per_step'])[:10]}
+    cpu = None
+    if not args.no_cpu_baseline:
+        # bounded sample: one fp32 train step of the oracle restatement on a
+        # 128x128x24 tile (same network, same step), scaled per voxel
+        from oracle import runet_oracle as ro, loss_oracle as lo
+        threads = max(1, min(16, os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        tile = (128, 128, 24)
+        st = ro.state_of(RDCNet(4, 5), torch.float32)
+        xs = host[0][:, :, :tile[0], :tile[1], :tile[2]].clone()
+        t1 = time.perf_counter()
+        o = ro.rdcnet_forward(st, xs)
+        ls = lo.cross_entropy(o[:, 0:1], mask[:, :, :tile[0], :tile[1], :tile[2]].cpu().float(),
+                              pwl[:, :, :tile[0], :tile[1], :tile[2]].cpu(), method='pixel') + \
+            lo.MSELoss(o[:, 2:], vec[:, :, :tile[0], :tile[1], :tile[2]].cpu())
+        ls.backward()
+        tt = time.perf_counter() - t1
+        cpu = {"value": tile[0] * tile[1] * tile[2] / tt, "unit": "voxels/s", "cores": threads, "kind": "port",
+               "sample": "1 train step (fwd+loss+bwd, no optimizer) of the oracle restatement of RDCNet "
+                         "(torch CPU fp32, %d threads) on a %s tile: %.2f s" % (threads, 'x'.join(map(str, tile)), tt)}
+    line = {"metric": "training voxels/sec (fwd+bwd+step), r_unet.py RDCNet, 512x512x24 tiles",
+            "value": vox / el, "unit": "voxels/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": "config 5: RDCNet(4, 5) train step (10 recurrent RDCBlock steps, "
+                                   "stacked dilations 1..5), B=1, 512x512x24x4 tiles from pinned host "
+                                   "memory with async prefetch, bf16 autocast",
+                       "final_loss": float(loss.item())},
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -298,9 +419,13 @@ def main():
                     help='clone the input every step (data-loader pattern; checks graph re-use)')
     ap.add_argument('--infer', action='store_true',
                     help='tiled inference driver throughput (SURVEY 8f-1) instead of training')
+    ap.add_argument('--runet', action='store_true',
+                    help='BASELINE config 5: r_unet.py RDCNet training on 512x512x24 tiles (bf16)')
     args = ap.parse_args()
     if args.infer:
         return infer_main(args)
+    if args.runet:
+        return runet_main(args)
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))

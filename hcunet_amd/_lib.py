@@ -123,6 +123,13 @@ SYMBOLS = [
     ("hcu_timing_disable", _I, []),
     ("hcu_timing_detail", _I, [_I]),
     ("hcu_timing_report", _I64, [ctypes.c_char_p, _I64]),
+    ("hcu_chain_plan_create", _I, [_VP, _I, _I, _I, _I, ctypes.POINTER(_VP)]),
+    ("hcu_chain_plan_query", _I, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I), ctypes.POINTER(_SZ),
+                                  ctypes.POINTER(_SZ)]),
+    ("hcu_chain_forward", _I, [_VP, ctypes.POINTER(UnetTensors), _I, _VP]),
+    ("hcu_chain_backward", _I, [_VP, ctypes.POINTER(UnetTensors), _VP, _VP, _I, _I, _VP]),
+    ("hcu_gate_fwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
+    ("hcu_gate_bwd", _I, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_tuning_set_mode", _I, [_I]),
     ("hcu_tuning_get_mode", _I, []),
     ("hcu_tuning_entries", _I64, [ctypes.POINTER(_I64)]),

@@ -686,6 +686,18 @@ struct PrepJob {
 constexpr int kPrepBatch = 32;   // jobs per launch: the batch is a kernel argument (< 4 KB)
 int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n, hipStream_t s);
 
+// Layer-chain layout kernels (layout.hip): dilation sub-lattices (space to
+// batch) and back, crop of a padded ConvTranspose3d output, NCXYZ output with
+// the last BatchNorm+ReLU applied.  es = element bytes (4 fp32, 2 bf16).
+int launch_s2b(const float *x, const float *sc, const float *sh, float *xs, int B, int X, int Y, int Z,
+               int Cs, int es, const int *D, const int *S, hipStream_t s);
+int launch_b2s(const float *ys, float *y, int B, int OX, int OY, int OZ, int Cs, int es, const int *D,
+               const int *S, hipStream_t s);
+int launch_crop_cl(const float *src, float *dst, int B, const int *sdims, const int *ddims, const int *off,
+                   int Cs, int es, hipStream_t s);
+int launch_from_cl_act(const float *y, const float *sc, const float *sh, float *out, int B, int C, int Cs,
+                       int64_t V, hipStream_t s, int bf);
+
 // Loss / optimizer (loss_adam.hip)
 int launch_loss_pixel(const float *pred, int B, int C, int PX, int PY, int PZ,
                       const void *mask, int mask_dtype, const void *pwl,

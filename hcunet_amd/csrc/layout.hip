@@ -1,0 +1,215 @@
+// Channels-last layout kernels of the layer-chain executor (unet.cpp,
+// hcu_chain_*): the dilation sub-lattice (space-to-batch) re-layouts that let a
+// large dilated Conv3d run as dilation-1 convolutions on its sub-grids
+// (hcat/r_unet.py:348-353: StackedDilation's 5^3 kernels at dilation 1..5),
+// the crop of a padded ConvTranspose3d output (nn.ConvTranspose3d(...,
+// padding=p), hcat/r_unet.py:216-217, 319-323), and the chain output in the
+// reference's NCXYZ layout with the last BatchNorm+ReLU applied.
+//
+// Every kernel moves 16-byte channel vectors (4 fp32 / 8 bf16 channels); the
+// channel stride Cs is a multiple of that vector.
+#include "common.h"
+#include "timing.h"
+
+namespace hcu {
+
+int layout_grid(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(g, 65536));
+}
+namespace {
+// relu(v * sc + sh) on one 16-byte vector of 4 fp32 / 8 bf16 channels
+__device__ __forceinline__ uint4 act16(uint4 v, const float *sc, const float *sh, int c0, bool bf) {
+  if (bf) {
+    float f[8];
+    unpack8(v, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[c0 + j], sh[c0 + j]), 0.f);
+    return pack8(f);
+  }
+  float4 f = __builtin_bit_cast(float4, v);
+  f.x = fmaxf(fmaf(f.x, sc[c0], sh[c0]), 0.f);
+  f.y = fmaxf(fmaf(f.y, sc[c0 + 1], sh[c0 + 1]), 0.f);
+  f.z = fmaxf(fmaf(f.z, sc[c0 + 2], sh[c0 + 2]), 0.f);
+  f.w = fmaxf(fmaf(f.w, sc[c0 + 3], sh[c0 + 3]), 0.f);
+  return __builtin_bit_cast(uint4, f);
+}
+}  // namespace
+
+// xs[(b*N + r)][x'][y'][z'] = act(x[b][rx + Dx x'][ry + Dy y'][rz + Dz z']) (0
+// outside x), r = (rx*Dy + ry)*Dz + rz, N = Dx*Dy*Dz; one 16-byte vector per
+// thread.  sc == nullptr: no activation.
+__global__ void __launch_bounds__(256)
+s2b_kernel(const uint4 *x, const float *sc, const float *sh, uint4 *xs, int X, int Y, int Z, int NV,
+           int Dx, int Dy, int Dz, int SX, int SY, int SZ, int64_t n, int bf) {
+  const int per = 16 / (bf ? 2 : 4);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int64_t q = i;
+    const int cv = (int)(q % NV); q /= NV;
+    const int z = (int)(q % SZ); q /= SZ;
+    const int y = (int)(q % SY); q /= SY;
+    const int xx = (int)(q % SX); q /= SX;
+    const int N = Dx * Dy * Dz;
+    const int r = (int)(q % N);
+    const int b = (int)(q / N);
+    const int rz = r % Dz, ry = (r / Dz) % Dy, rx = r / (Dz * Dy);
+    const int gx = rx + Dx * xx, gy = ry + Dy * y, gz = rz + Dz * z;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (gx < X && gy < Y && gz < Z) {
+      v = x[(((int64_t)b * X + gx) * Y + gy) * (int64_t)Z * NV + (int64_t)gz * NV + cv];
+      if (sc) v = act16(v, sc, sh, cv * per, bf != 0);
+    }
+    xs[i] = v;
+  }
+}
+
+// y[b][o] = ys[(b*N + r)][o'] for every output voxel o = r + D o' (< OX, OY, OZ).
+__global__ void __launch_bounds__(256)
+b2s_kernel(const uint4 *ys, uint4 *y, int OX, int OY, int OZ, int NV, int Dx, int Dy, int Dz,
+           int SX, int SY, int SZ, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int64_t q = i;
+    const int cv = (int)(q % NV); q /= NV;
+    const int oz = (int)(q % OZ); q /= OZ;
+    const int oy = (int)(q % OY); q /= OY;
+    const int ox = (int)(q % OX);
+    const int b = (int)(q / OX);
+    const int r = ((ox % Dx) * Dy + oy % Dy) * Dz + oz % Dz;
+    const int64_t bs = (int64_t)b * Dx * Dy * Dz + r;
+    y[i] = ys[(((bs * SX + ox / Dx) * SY + oy / Dy) * SZ + oz / Dz) * NV + cv];
+  }
+}
+
+// dst[b][x][y][z] = src[b][x + ox][y + oy][z + oz] (channels-last box copy).
+__global__ void __launch_bounds__(256)
+crop_kernel(const uint4 *src, uint4 *dst, int SX, int SY, int SZ, int DX, int DY, int DZ, int NV,
+            int ox, int oy, int oz, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    int64_t q = i;
+    const int cv = (int)(q % NV); q /= NV;
+    const int z = (int)(q % DZ); q /= DZ;
+    const int y = (int)(q % DY); q /= DY;
+    const int x = (int)(q % DX);
+    const int b = (int)(q / DX);
+    dst[i] = src[((((int64_t)b * SX + x + ox) * SY + y + oy) * SZ + z + oz) * NV + cv];
+  }
+}
+
+// out[b][c][v] = act(y[b][v][c]) (NCXYZ fp32; act = relu(y*sc + sh) or identity).
+template <bool BF>
+__global__ void __launch_bounds__(256)
+from_cl_act_kernel(const void *y, const float *sc, const float *sh, float *out, int C, int Cs, int64_t V,
+                   int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t v = i % V, q = i / V;
+    const int c = (int)(q % C);
+    const int64_t b = q / C;
+    const int64_t src = (b * V + v) * Cs + c;
+    float f = BF ? bf2f(reinterpret_cast<const uint16_t *>(y)[src]) : reinterpret_cast<const float *>(y)[src];
+    if (sc) f = fmaxf(fmaf(f, sc[c], sh[c]), 0.f);
+    out[i] = f;
+  }
+}
+
+int launch_s2b(const float *x, const float *sc, const float *sh, float *xs, int B, int X, int Y, int Z,
+               int Cs, int es, const int *D, const int *S, hipStream_t s) {
+  const int NV = Cs * es / 16;
+  const int64_t n = (int64_t)B * D[0] * D[1] * D[2] * S[0] * S[1] * S[2] * NV;
+  HCU_TIMED(s, "s2b_kernel", 0.0, 16.0 * n * 2,
+            hipLaunchKernelGGL(s2b_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)x, sc, sh,
+                               (uint4 *)xs, X, Y, Z, NV, D[0], D[1], D[2], S[0], S[1], S[2], n, es == 2));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_b2s(const float *ys, float *y, int B, int OX, int OY, int OZ, int Cs, int es, const int *D,
+               const int *S, hipStream_t s) {
+  const int NV = Cs * es / 16;
+  const int64_t n = (int64_t)B * OX * OY * OZ * NV;
+  HCU_TIMED(s, "b2s_kernel", 0.0, 16.0 * n * 2,
+            hipLaunchKernelGGL(b2s_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)ys, (uint4 *)y,
+                               OX, OY, OZ, NV, D[0], D[1], D[2], S[0], S[1], S[2], n));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_crop_cl(const float *src, float *dst, int B, const int *sdims, const int *ddims, const int *off,
+                   int Cs, int es, hipStream_t s) {
+  const int NV = Cs * es / 16;
+  const int64_t n = (int64_t)B * ddims[0] * ddims[1] * ddims[2] * NV;
+  HCU_TIMED(s, "crop_kernel", 0.0, 16.0 * n * 2,
+            hipLaunchKernelGGL(crop_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)src,
+                               (uint4 *)dst, sdims[0], sdims[1], sdims[2], ddims[0], ddims[1], ddims[2], NV,
+                               off[0], off[1], off[2], n));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_from_cl_act(const float *y, const float *sc, const float *sh, float *out, int B, int C, int Cs,
+                       int64_t V, hipStream_t s, int bf) {
+  const int64_t n = (int64_t)B * C * V;
+  if (bf)
+    HCU_TIMED(s, "from_cl_act_kernel", 0.0, 6.0 * n,
+              hipLaunchKernelGGL(from_cl_act_kernel<true>, dim3(layout_grid(n)), dim3(256), 0, s, (const void *)y,
+                                 sc, sh, out, C, Cs, V, n));
+  else
+    HCU_TIMED(s, "from_cl_act_kernel", 0.0, 8.0 * n,
+              hipLaunchKernelGGL(from_cl_act_kernel<false>, dim3(layout_grid(n)), dim3(256), 0, s,
+                                 (const void *)y, sc, sh, out, C, Cs, V, n));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu
+
+// ---------------------------------------------------------------------------
+// The gated recurrence of RecursiveUnet.forward (hcat/r_unet.py:150-155):
+//   h = tanh(hp), z = sigmoid(zp), out = h_prev * z + (-1 * z * h)
+// (h_prev == nullptr: ones, the t == 0 state, :152-153) and its gradient.
+namespace hcu {
+__device__ __forceinline__ float sigm(float v) { return 1.f / (1.f + expf(-v)); }
+
+__global__ void __launch_bounds__(256)
+gate_fwd_kernel(const float *hp, const float *zp, const float *hprev, float *out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float h = tanhf(hp[i]), z = sigm(zp[i]);
+    const float hv = hprev ? hprev[i] : 1.f;
+    out[i] = hv * z + (-1.f * z * h);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+gate_bwd_kernel(const float *hp, const float *zp, const float *hprev, const float *dout, float *dhp,
+                float *dzp, float *dhprev, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float h = tanhf(hp[i]), z = sigm(zp[i]);
+    const float hv = hprev ? hprev[i] : 1.f;
+    const float g = dout[i];
+    if (dhprev) dhprev[i] = g * z;
+    dzp[i] = g * (hv - h) * (z * (1.f - z));
+    dhp[i] = -g * z * (1.f - h * h);
+  }
+}
+}  // namespace hcu
+
+extern "C" {
+int hcu_gate_fwd(const float *hp, const float *zp, const float *hprev, float *out, int64_t n, void *stream) {
+  if (!hp || !zp || !out || n < 0) return hcu::fail(1, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  HCU_TIMED(s, "gate_fwd_kernel", 0.0, 16.0 * n,
+            hipLaunchKernelGGL(hcu::gate_fwd_kernel, dim3(hcu::layout_grid(n)), dim3(256), 0, s, hp, zp, hprev,
+                               out, n));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+int hcu_gate_bwd(const float *hp, const float *zp, const float *hprev, const float *dout, float *dhp,
+                 float *dzp, float *dhprev, int64_t n, void *stream) {
+  if (!hp || !zp || !dout || !dhp || !dzp || n < 0) return hcu::fail(1, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  HCU_TIMED(s, "gate_bwd_kernel", 0.0, 28.0 * n,
+            hipLaunchKernelGGL(hcu::gate_bwd_kernel, dim3(hcu::layout_grid(n)), dim3(256), 0, s, hp, zp, hprev,
+                               dout, dhp, dzp, dhprev, n));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+}  // extern "C"

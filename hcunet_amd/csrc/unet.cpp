@@ -87,6 +87,15 @@ struct ConvLayer {
   std::string name;  // layer tag for per-layer timing ("d0.c1", "u3.c2", ...)
   int Cout = 0, Cin_g = 0, groups = 1, fold_mod = 0, E = 0, T = 0;
   int K[3], D[3];
+  int S[3] = {1, 1, 1}, P[3] = {0, 0, 0};   // stride, zero padding (chains; the U-Net is valid)
+  bool has_dgrad = true;                   // input gradient planned (stride 1)
+  // Dilated convolution run on the dilation sub-lattices (space-to-batch):
+  // when the dilated halo does not fit the conv kernels' LDS, the input is
+  // re-laid as dx*dy*dz dense sub-grids [B*D][X'][Y'][Z'] and fwd / dgrad /
+  // wgrad are planned as dilation-1 convolutions on them (padding P/D).
+  bool s2b = false;
+  int L3[3] = {1, 1, 1};                   // lattice (= D) of the s2b form
+  Dims sub_in, sub_out;                    // sub-grid tensors (batch B*D)
   int64_t w_off = 0, b_off = 0;
   Dims in, out;
   GConvArgs fwd{}, dgrad{};
@@ -167,13 +176,119 @@ WGradArgs wgrad_conv(const Dims &in, const Dims &out, const int K[3], const int 
   return w;
 }
 
+// Conv3d with stride / zero padding (nn.Conv3d(..., stride, padding), the
+// r_unet.py layers): out = floor((in + 2P - D(K-1) - 1) / S) + 1.  Forward:
+// o*S + t*D - P; input gradient (stride 1): the full correlation with padding
+// D(K-1) - P; weight gradient: A offset o*S + t*D - P.  A dilated kernel whose
+// halo does not fit the kernels' LDS runs on the dilation sub-lattices (s2b).
+int setup_conv_general(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
+                       int cin_total, const char *name) {
+  if (groups < 1 || cin_total % groups || Cout % groups)
+    return fail(HCU_ERR_INVALID, std::string(name) + ": channels must be divisible by groups");
+  L.Cout = Cout;
+  L.groups = groups;
+  L.Cin_g = cin_total / groups;
+  L.fold_mod = fold_mod;
+  L.E = std::min(fold_mod, cin_total);
+  L.T = L.K[0] * L.K[1] * L.K[2];
+  L.in = in;
+  int o[3];
+  const int iv[3] = {in.X, in.Y, in.Z};
+  for (int i = 0; i < 3; ++i) {
+    const int span = iv[i] + 2 * L.P[i] - L.D[i] * (L.K[i] - 1);
+    if (span < 1)
+      return fail(HCU_ERR_SHAPE, std::string(name) + ": Calculated padded input size per channel: (" +
+                                     std::to_string(in.X + 2 * L.P[0]) + " x " + std::to_string(in.Y + 2 * L.P[1]) +
+                                     " x " + std::to_string(in.Z + 2 * L.P[2]) +
+                                     "). Kernel size can't be greater than actual input size");
+    o[i] = (span - 1) / L.S[i] + 1;
+  }
+  L.out = mkdims(in.B, o[0], o[1], o[2], Cout, in.es);
+  const bool bf = in.es == 2;
+  auto plan_c = [&](GConvArgs &a) { return bf ? plan_bconv(a, kTargetBlocks) : plan_conv_fp32(a, kTargetBlocks); };
+  L.has_dgrad = L.S[0] == 1 && L.S[1] == 1 && L.S[2] == 1;
+  L.s2b = false;
+  // direct form
+  {
+    GConvArgs f = gconv_conv_fwd(in, L.out, L.K, L.D, Cout);
+    f.sx = L.S[0]; f.sy = L.S[1]; f.sz = L.S[2];
+    f.px = L.P[0]; f.py = L.P[1]; f.pz = L.P[2];
+    const int ef = plan_c(f);
+    int ed = 0;
+    GConvArgs dg{};
+    if (L.has_dgrad) {
+      dg = gconv_conv_dgrad(in, L.out, L.K, L.D, L.E);
+      dg.px = L.D[0] * (L.K[0] - 1) - L.P[0];
+      dg.py = L.D[1] * (L.K[1] - 1) - L.P[1];
+      dg.pz = L.D[2] * (L.K[2] - 1) - L.P[2];
+      if (dg.px < 0 || dg.py < 0 || dg.pz < 0)
+        return fail(HCU_ERR_UNSUPPORTED, std::string(name) + ": padding larger than dilation*(kernel-1)");
+      ed = plan_c(dg);
+    }
+    WGradArgs w = wgrad_conv(in, L.out, L.K, L.D);
+    w.asx = L.S[0]; w.asy = L.S[1]; w.asz = L.S[2];
+    w.apx = L.P[0]; w.apy = L.P[1]; w.apz = L.P[2];
+    const int ew = bf ? plan_bwgrad(w, kTargetBlocks) : plan_wgrad(w, kTargetBlocks);
+    const bool dil = L.D[0] > 1 || L.D[1] > 1 || L.D[2] > 1;
+    if (!ef && !ed && !ew) {
+      L.fwd = f;
+      L.dgrad = dg;
+      L.wg = w;
+    } else if (!dil || !L.has_dgrad) {
+      return ef ? ef : ed ? ed : ew;
+    } else {
+      L.s2b = true;
+    }
+  }
+  if (L.s2b) {
+    // dilation sub-lattices: output o = r + D*o' reads input r + D*(o' + t - P/D)
+    int sub_i[3], sub_o[3], Pd[3];
+    const int one[3] = {1, 1, 1};
+    int nlat = 1;
+    for (int i = 0; i < 3; ++i) {
+      if (L.P[i] % L.D[i])
+        return fail(HCU_ERR_UNSUPPORTED, std::string(name) + ": dilated convolution too large for one tile "
+                                                             "and padding not a multiple of the dilation");
+      L.L3[i] = L.D[i];
+      nlat *= L.D[i];
+      Pd[i] = L.P[i] / L.D[i];
+      sub_i[i] = cdiv(iv[i], L.D[i]);
+      sub_o[i] = sub_i[i] + 2 * Pd[i] - (L.K[i] - 1);
+      if (sub_o[i] < cdiv(o[i], L.D[i]))
+        return fail(HCU_ERR_UNSUPPORTED, std::string(name) + ": sub-lattice output too small");
+    }
+    L.sub_in = mkdims(in.B * nlat, sub_i[0], sub_i[1], sub_i[2], in.C, in.es);
+    L.sub_out = mkdims(in.B * nlat, sub_o[0], sub_o[1], sub_o[2], Cout, in.es);
+    L.fwd = gconv_conv_fwd(L.sub_in, L.sub_out, L.K, one, Cout);
+    L.fwd.px = Pd[0]; L.fwd.py = Pd[1]; L.fwd.pz = Pd[2];
+    if (int e = plan_c(L.fwd)) return e;
+    L.dgrad = gconv_conv_dgrad(L.sub_in, L.sub_out, L.K, one, L.E);
+    L.dgrad.px = (L.K[0] - 1) - Pd[0];
+    L.dgrad.py = (L.K[1] - 1) - Pd[1];
+    L.dgrad.pz = (L.K[2] - 1) - Pd[2];
+    if (int e = plan_c(L.dgrad)) return e;
+    L.wg = wgrad_conv(L.sub_in, L.sub_out, L.K, one);
+    L.wg.apx = Pd[0]; L.wg.apy = Pd[1]; L.wg.apz = Pd[2];
+    if (int e = bf ? plan_bwgrad(L.wg, kTargetBlocks) : plan_wgrad(L.wg, kTargetBlocks)) return e;
+  }
+  L.bn.C = Cout;
+  L.bn.Cs = L.out.Cs;
+  L.bn.count = (double)L.out.vox();
+  return 0;
+}
+
 int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod, int cin_total,
-               const int K[3], const int D[3], const char *name) {
+               const int K[3], const int D[3], const char *name, const int *S = nullptr,
+               const int *P = nullptr) {
   for (int i = 0; i < 3; ++i) {
     L.K[i] = K[i];
     L.D[i] = D[i];
+    L.S[i] = S ? S[i] : 1;
+    L.P[i] = P ? P[i] : 0;
     if (K[i] < 1 || D[i] < 1) return fail(HCU_ERR_INVALID, std::string(name) + ": bad kernel/dilation");
+    if (L.S[i] < 1 || L.P[i] < 0) return fail(HCU_ERR_INVALID, std::string(name) + ": bad stride/padding");
   }
+  if (S || P) return setup_conv_general(L, in, Cout, groups, fold_mod, cin_total, name);
   if (groups < 1 || cin_total % groups || Cout % groups)
     return fail(HCU_ERR_INVALID, std::string(name) + ": channels must be divisible by groups");
   L.Cout = Cout;
@@ -347,6 +462,23 @@ struct hcu_unet_plan {
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
   size_t fin_off = 0;   // fused BatchNorm finalize ticket counter (zeroed per forward)
   double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
+  // Layer-chain plans (hcu_chain_*): a sequence of ops instead of the U-Net.
+  struct ChainOp {
+    int kind = 0;                  // HCU_CHAIN_CONV / POOL / CONVT
+    bool bn_relu = false, fold = false;
+    ConvLayer conv;
+    ConvTLayer ct;
+    int pk[3] = {1, 1, 1};
+    Dims pooled;
+    size_t pool_off = 0;
+    int crop[3] = {0, 0, 0};       // ConvTranspose3d padding: crop of the full output
+    Dims ufull;
+    size_t xs_off = 0;             // s2b conv: the sub-lattice input (saved for the weight gradient)
+  };
+  std::vector<ChainOp> chain;
+  bool is_chain = false;
+  size_t ufull_off = 0, sub_off[3] = {};   // scratch: full ConvTranspose3d output, sub-lattice temporaries
+  size_t max_sub = 0, max_ufull = 0;
   size_t wpart_floats = 0;   // weight-gradient slab arena (deferred, batched finalizes)
   size_t max_act = 0, max_part = 0, max_wprep = 0, max_kpart = 0;
   // Captured launch sequences (hipGraph) keyed by the buffers they bake in:
@@ -735,7 +867,7 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   a.in_scale = isc;
   a.in_shift = ish;
   a.w = c.fptr(c.sv, L.wf_off);
-  a.bias = c.P + L.b_off;
+  a.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
   a.out = c.fptr(c.sv, L.y_off);
   a.stats = training ? c.part() : nullptr;
   a.partial = c.kpart();
@@ -830,7 +962,7 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   WGradFinalize f{};
   f.partial = w.partial;
   f.dw = c.G + L.w_off;
-  f.db = c.G + L.b_off;
+  f.db = L.b_off >= 0 ? c.G + L.b_off : nullptr;
   f.KB = w.KB;
   f.Mtot = w.Mtot;
   f.Ntot = w.Ntot;
@@ -1194,6 +1326,12 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   c.split = split;
   c.ws = split ? p.side : c.s;
+  // an eval-mode forward prepared only the forward weight images: the
+  // input-gradient images are laid out here
+  if (!training && !p.prep_bwd.empty())
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(),
+                                c.s))
+      return e;
   int cur = 0;  // slot holding the current d(pre-BN y)
   if (int e = c.alloc(cur)) return e;
 
@@ -1657,6 +1795,538 @@ int hcu_adam_step(float *p, const float *g, float *m, float *v, int64_t n, float
                   hcu_stream_t stream) {
   return launch_adam(p, g, m, v, n, lr, beta1, beta2, eps, weight_decay, step, grad_scale,
                      (hipStream_t)stream);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Layer chains (include/hcunet.h, hcu_chain_*): a sequence of Conv3d [+ BN +
+// ReLU] / MaxPool3d / ConvTranspose3d [+ cat(U, U)] ops with the network
+// executor's kernels and fusions: BatchNorm+ReLU applied while the consumer
+// stages its operand, BatchNorm statistics in the producing conv's epilogue,
+// the BatchNorm backward reduction in the consumer dgrad's epilogue or fused
+// with the max-pool backward.  Single stream, direct launches.
+// ---------------------------------------------------------------------------
+namespace {
+
+using ChainOp = hcu_unet_plan::ChainOp;
+
+int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
+  if (cs.n_ops < 1 || cs.n_ops > HCU_CHAIN_MAX_OPS) return fail(HCU_ERR_INVALID, "chain: 1..16 ops");
+  if (cs.compute_dtype != HCU_F32 && cs.compute_dtype != HCU_BF16)
+    return fail(HCU_ERR_INVALID, "compute_dtype must be HCU_F32 or HCU_BF16");
+  if (cs.in_channels < 1) return fail(HCU_ERR_INVALID, "chain: in_channels must be positive");
+  if (p.B < 1 || p.X < 1 || p.Y < 1 || p.Z < 1) return fail(HCU_ERR_SHAPE, "empty input");
+  p.is_chain = true;
+  p.L = 0;
+  p.es = cs.compute_dtype == HCU_BF16 ? 2 : 4;
+  p.spec = hcu_unet_spec{};
+  p.spec.bn_eps = cs.bn_eps;
+  p.spec.bn_momentum = cs.bn_momentum;
+  p.spec.compute_dtype = cs.compute_dtype;
+  const bool bf = p.es == 2;
+  Region saved;
+  p.xin = mkdims(p.B, p.X, p.Y, p.Z, cs.in_channels, p.es);
+  p.xcl_off = saved.take_floats(p.xin.floats());
+  p.max_act = p.xin.floats();
+  p.chain.assign(cs.n_ops, ChainOp{});
+  Dims cur = p.xin;
+  int prev = -1;
+  bool prev_bn = false;
+  int bn_index = 0;
+  for (int i = 0; i < cs.n_ops; ++i) {
+    const hcu_chain_op &s = cs.ops[i];
+    ChainOp &o = p.chain[i];
+    o.kind = s.kind;
+    const std::string nm = "c" + std::to_string(i);
+    if (s.kind == HCU_CHAIN_CONV) {
+      o.bn_relu = s.bn_relu != 0;
+      o.fold = s.cat_fold != 0;
+      if (o.fold && prev != HCU_CHAIN_CONVT)
+        return fail(HCU_ERR_INVALID, "chain: cat_fold needs a preceding ConvTranspose3d");
+      const int cin_total = o.fold ? 2 * cur.C : cur.C;
+      const int fold_mod = o.fold ? cur.C : cin_total;
+      ConvLayer &L = o.conv;
+      L.name = nm;
+      if (int e = setup_conv(L, cur, s.out_channels, s.groups, fold_mod, cin_total, s.k, s.dil, "Conv3d",
+                             s.stride, s.pad))
+        return e;
+      if (L.s2b && o.bn_relu)
+        return fail(HCU_ERR_UNSUPPORTED, "chain: BatchNorm after a sub-lattice (large dilated) Conv3d");
+      L.w_off = s.w_off;
+      L.b_off = s.b_off;
+      if (L.s2b) {
+        o.xs_off = saved.take_floats(L.sub_in.floats());
+        p.max_sub = std::max({p.max_sub, L.sub_in.floats(), L.sub_out.floats()});
+      }
+      L.y_off = saved.take_floats(L.out.floats());
+      if (o.bn_relu) {
+        L.bn.coef_off = saved.take_floats((size_t)6 * L.bn.Cs);
+        L.bn.gamma = s.gamma_off;
+        L.bn.beta = s.beta_off;
+        L.bn.index = bn_index++;
+      }
+      track_conv(p, L);
+      cur = L.out;
+      prev_bn = o.bn_relu;
+    } else if (s.kind == HCU_CHAIN_POOL) {
+      if (!(prev == HCU_CHAIN_CONV && prev_bn))
+        return fail(HCU_ERR_UNSUPPORTED, "chain: MaxPool3d must follow Conv3d + BatchNorm3d + ReLU");
+      for (int d = 0; d < 3; ++d) {
+        o.pk[d] = s.k[d];
+        if (s.k[d] < 1) return fail(HCU_ERR_INVALID, "chain: bad pool kernel");
+      }
+      const int px = cur.X / o.pk[0], py = cur.Y / o.pk[1], pz = cur.Z / o.pk[2];
+      if (px < 1 || py < 1 || pz < 1) return fail(HCU_ERR_SHAPE, "max_pool3d: Output size is too small");
+      o.pooled = mkdims(p.B, px, py, pz, cur.C, p.es);
+      o.pool_off = saved.take_floats(o.pooled.floats());
+      p.max_act = std::max(p.max_act, o.pooled.floats());
+      cur = o.pooled;
+      prev_bn = false;
+    } else if (s.kind == HCU_CHAIN_CONVT) {
+      for (int d = 0; d < 3; ++d)
+        if (s.dil[d] > 1) return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d: dilation must be 1");
+      if (s.groups > 1) return fail(HCU_ERR_UNSUPPORTED, "ConvTranspose3d: groups must be 1");
+      ConvTLayer &u = o.ct;
+      u.name = nm;
+      if (int e = setup_convt(u, cur, s.out_channels, s.k, s.stride, p.max_wprep, p.max_part, p.max_kpart))
+        return e;
+      u.w_off = s.w_off;
+      u.b_off = s.b_off;
+      const Dims full = u.out;
+      int cd[3];
+      const int fd[3] = {full.X, full.Y, full.Z};
+      bool crop = false;
+      for (int d = 0; d < 3; ++d) {
+        o.crop[d] = s.pad[d];
+        if (s.pad[d] < 0) return fail(HCU_ERR_INVALID, "ConvTranspose3d: negative padding");
+        cd[d] = fd[d] - 2 * s.pad[d];
+        if (cd[d] < 1) return fail(HCU_ERR_SHAPE, "ConvTranspose3d: output size is too small");
+        crop = crop || s.pad[d] > 0;
+      }
+      if (crop) {
+        // forward: full output into scratch, then the crop; backward: the
+        // cropped gradient read at offset pad (zero outside it)
+        o.ufull = full;
+        p.max_ufull = std::max(p.max_ufull, full.floats());
+        u.out = mkdims(p.B, cd[0], cd[1], cd[2], s.out_channels, p.es);
+        GConvArgs &a = u.dgrad;
+        a.use_bconv = a.use_conv2 = a.use_conv8 = 0;   // re-planned from scratch
+        a.bes = 0;
+        a.IX = cd[0]; a.IY = cd[1]; a.IZ = cd[2];
+        a.px = s.pad[0]; a.py = s.pad[1]; a.pz = s.pad[2];
+        if (int e = bf ? plan_bconv(a, kTargetBlocks) : plan_conv_fp32(a, kTargetBlocks)) return e;
+        p.max_wprep = std::max(p.max_wprep, wprep_floats(a));
+        p.max_part = std::max(p.max_part, (size_t)gconv_rows(a) * a.CoutW * 2);
+        p.max_kpart = std::max(p.max_kpart, conv_partial_floats(a));
+        WGradArgs &w = u.wg;
+        w.v2 = 0;
+        w.use_bw = 0;
+        w.GX = cd[0]; w.GY = cd[1]; w.GZ = cd[2];
+        w.gpx = s.pad[0]; w.gpy = s.pad[1]; w.gpz = s.pad[2];
+        if (int e = bf ? plan_bwgrad(w, kTargetBlocks) : plan_wgrad(w, kTargetBlocks)) return e;
+        p.max_part = std::max(p.max_part, wgrad_partial_floats(w));
+        p.max_part = std::max(p.max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
+      }
+      u.u_off = saved.take_floats(u.out.floats());
+      p.max_act = std::max(p.max_act, u.out.floats());
+      cur = u.out;
+      prev_bn = false;
+    } else {
+      return fail(HCU_ERR_INVALID, "chain: unknown op kind");
+    }
+    prev = s.kind;
+  }
+  p.outd = cur;
+  p.n_bn = bn_index;
+  // weight re-layouts (one batched launch per forward)
+  p.prep_jobs.clear();
+  auto add_job = [&](int kind, size_t n, int64_t src, const WPack &pk, const int *prm, int np, size_t &off) {
+    PrepJob j{};
+    j.kind = kind;
+    j.bf16 = bf;
+    j.n = (int64_t)n;
+    j.src = src;
+    off = saved.take_floats(j.bf16 ? (n + 1) / 2 : n);
+    j.dst = (int64_t)(off / sizeof(float));
+    j.pk = pk;
+    std::copy(prm, prm + np, j.p);
+    p.prep_jobs.push_back(j);
+  };
+  for (ChainOp &o : p.chain) {
+    if (o.kind == HCU_CHAIN_CONV) {
+      ConvLayer &cl = o.conv;
+      const int pf[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.fwd.ICs, cl.fwd.CoutW,
+                         std::min(cl.fold_mod, cl.groups * cl.Cin_g)};
+      add_job(PREP_CONV_FWD, prep_elems(cl.fwd), cl.w_off, wpack_of(cl.fwd), pf, 8, cl.wf_off);
+      if (cl.has_dgrad) {
+        const int pd[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.dgrad.ICs, cl.dgrad.CoutW, cl.E};
+        add_job(PREP_CONV_DGRAD, prep_elems(cl.dgrad), cl.w_off, wpack_of(cl.dgrad), pd, 8, cl.wd_off);
+      }
+    } else if (o.kind == HCU_CHAIN_CONVT) {
+      ConvTLayer &u = o.ct;
+      if (u.fused) {
+        const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
+                            u.fwdf.ICs, u.fwdf.CoutW};
+        add_job(PREP_CONVT_FUSED, prep_elems(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 10, u.wf_off);
+      } else {
+        u.wph_off.assign(u.phases.size(), 0);
+        for (size_t ph = 0; ph < u.phases.size(); ++ph) {
+          const int *pj = &u.pJ[ph * 6];
+          const GConvArgs &a = u.phases[ph];
+          const int pf[16] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
+                              pj[0], pj[1], pj[2], pj[3], pj[4], pj[5], a.ICs, a.CoutW};
+          add_job(PREP_CONVT_PHASE, (size_t)pj[3] * pj[4] * pj[5] * a.ICs * a.CoutW, u.w_off, WPack{}, pf,
+                  16, u.wph_off[ph]);
+        }
+      }
+      const int pd[5] = {u.Cin, u.Cout, u.T, u.dgrad.ICs, u.dgrad.CoutW};
+      add_job(PREP_CONVT_DGRAD, prep_elems(u.dgrad), u.w_off, wpack_of(u.dgrad), pd, 5, u.wd_off);
+    }
+  }
+  p.prep_fwd.clear();
+  p.prep_bwd.clear();
+  for (const PrepJob &j : p.prep_jobs)
+    (j.kind == PREP_CONV_DGRAD || j.kind == PREP_CONVT_DGRAD ? p.prep_bwd : p.prep_fwd).push_back(j);
+  p.saved_bytes = saved.off;
+  Region scratch;
+  for (size_t &b : p.buf_off) b = scratch.take_floats(p.max_act);
+  p.part_off = scratch.take_floats(p.max_part);
+  p.wpart_floats = std::max<size_t>(p.max_part, (size_t)1 << 20);
+  p.wpart_off = scratch.take_floats(p.wpart_floats);
+  p.wprep_off = scratch.take_floats(p.max_wprep);
+  p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
+  p.fin_off = scratch.take_floats(16);
+  p.ufull_off = scratch.take_floats(p.max_ufull);
+  for (size_t &o : p.sub_off) o = scratch.take_floats(p.max_sub);
+  p.scratch_bytes = scratch.off;
+  return 0;
+}
+
+// Activation entering each op: (tensor, BatchNorm scale, shift) -- the
+// producer's BatchNorm+ReLU is applied by the consumer while it loads.
+struct ChainAct {
+  const float *x = nullptr, *sc = nullptr, *sh = nullptr;
+};
+
+std::vector<ChainAct> chain_inputs(const hcu_unet_plan &p, char *sv, ChainAct *out_act) {
+  std::vector<ChainAct> in(p.chain.size());
+  ChainAct a;
+  a.x = reinterpret_cast<const float *>(sv + p.xcl_off);
+  for (size_t i = 0; i < p.chain.size(); ++i) {
+    const ChainOp &o = p.chain[i];
+    in[i] = a;
+    if (o.kind == HCU_CHAIN_CONV) {
+      a.x = reinterpret_cast<const float *>(sv + o.conv.y_off);
+      if (o.bn_relu) {
+        const BNCoef cf = coef_at(sv, o.conv.bn);
+        a.sc = cf.scale;
+        a.sh = cf.shift;
+      } else {
+        a.sc = a.sh = nullptr;
+      }
+    } else if (o.kind == HCU_CHAIN_POOL) {
+      a = ChainAct{reinterpret_cast<const float *>(sv + o.pool_off), nullptr, nullptr};
+    } else {
+      a = ChainAct{reinterpret_cast<const float *>(sv + o.ct.u_off), nullptr, nullptr};
+    }
+  }
+  if (out_act) *out_act = a;
+  return in;
+}
+
+int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training, hipStream_t s) {
+  Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  const int es = p.es, bf = c.bf();
+  float *xcl = c.fptr(c.sv, p.xcl_off);
+  tag(std::string("chain"), "fwd");
+  if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf, t->x_dtype)) return e;
+  const std::vector<PrepJob> &jobs = training ? p.prep_jobs : p.prep_fwd;
+  if (!jobs.empty())
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), jobs.data(), (int)jobs.size(), s)) return e;
+  ChainAct last;
+  const std::vector<ChainAct> in = chain_inputs(p, c.sv, &last);
+  for (size_t i = 0; i < p.chain.size(); ++i) {
+    const ChainOp &o = p.chain[i];
+    const ChainAct &a = in[i];
+    if (o.kind == HCU_CHAIN_CONV) {
+      const ConvLayer &L = o.conv;
+      float *y = c.fptr(c.sv, L.y_off);
+      if (L.s2b) {
+        float *xs = c.fptr(c.sv, o.xs_off), *ys = c.fptr(c.sc, p.sub_off[0]);
+        const int sd[3] = {L.sub_in.X, L.sub_in.Y, L.sub_in.Z}, so[3] = {L.sub_out.X, L.sub_out.Y, L.sub_out.Z};
+        tag(L.name, "fwd");
+        if (int e = launch_s2b(a.x, a.sc, a.sh, xs, p.B, L.in.X, L.in.Y, L.in.Z, L.in.Cs, es, L.L3, sd, s))
+          return e;
+        GConvArgs g = L.fwd;
+        g.in = xs;
+        g.in_scale = g.in_shift = nullptr;
+        g.w = c.fptr(c.sv, L.wf_off);
+        g.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
+        g.out = ys;
+        g.stats = nullptr;
+        g.partial = c.kpart();
+        if (int e = launch_conv_any(g, s)) return e;
+        if (int e = launch_b2s(ys, y, p.B, L.out.X, L.out.Y, L.out.Z, L.out.Cs, es, L.L3, so, s)) return e;
+      } else if (o.bn_relu) {
+        if (int e = conv_forward(c, L, a.x, a.sc, a.sh, training)) return e;
+      } else {
+        tag(L.name, "fwd");
+        GConvArgs g = L.fwd;
+        g.in = a.x;
+        g.in_scale = a.sc;
+        g.in_shift = a.sh;
+        g.w = c.fptr(c.sv, L.wf_off);
+        g.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
+        g.out = y;
+        g.stats = nullptr;
+        g.partial = c.kpart();
+        if (int e = launch_conv_any(g, s)) return e;
+      }
+    } else if (o.kind == HCU_CHAIN_POOL) {
+      const ConvLayer &P = p.chain[i - 1].conv;
+      tag(P.name, "pool");
+      if (int e = launch_maxpool_fwd(a.x, a.sc, a.sh, c.fptr(c.sv, o.pool_off), p.B, P.out.X, P.out.Y,
+                                     P.out.Z, P.out.Cs, o.pk[0], o.pk[1], o.pk[2], s, bf))
+        return e;
+    } else {
+      const ConvTLayer &u = o.ct;
+      tag(u.name, "fwd");
+      const bool crop = o.crop[0] || o.crop[1] || o.crop[2];
+      float *U = crop ? c.fptr(c.sc, p.ufull_off) : c.fptr(c.sv, u.u_off);
+      const float *bias = u.b_off >= 0 ? c.P + u.b_off : nullptr;
+      if (u.fused) {
+        GConvArgs g = u.fwdf;
+        g.in = a.x;
+        g.in_scale = a.sc;
+        g.in_shift = a.sh;
+        g.w = c.fptr(c.sv, u.wf_off);
+        g.bias = bias;
+        g.out = U;
+        g.stats = nullptr;
+        g.partial = c.kpart();
+        if (int e = launch_conv_any(g, s)) return e;
+      }
+      for (size_t ph = 0; !u.fused && ph < u.phases.size(); ++ph) {
+        GConvArgs g = u.phases[ph];
+        g.in = a.x;
+        g.in_scale = a.sc;
+        g.in_shift = a.sh;
+        g.w = c.fptr(c.sv, u.wph_off[ph]);
+        g.bias = bias;
+        g.out = U;
+        g.stats = nullptr;
+        if (int e = launch_gconv(g, s)) return e;
+      }
+      if (crop) {
+        const int sd[3] = {o.ufull.X, o.ufull.Y, o.ufull.Z}, dd[3] = {u.out.X, u.out.Y, u.out.Z};
+        if (int e = launch_crop_cl(U, c.fptr(c.sv, u.u_off), p.B, sd, dd, o.crop, u.out.Cs, es, s)) return e;
+      }
+    }
+  }
+  tag(std::string("chain"), "out");
+  if (int e = launch_from_cl_act(last.x, last.sc, last.sh, t->out, p.B, p.outd.C, p.outd.Cs,
+                                 p.outd.vox() / p.B, s, bf))
+    return e;
+  if (training && p.n_bn && t->bn_num_batches_tracked)
+    if (int e = launch_bn_count_increment(t->bn_num_batches_tracked, p.n_bn, s)) return e;
+  if (timing_on()) timing_set_tag("");
+  return HCU_OK;
+}
+
+int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout, float *dx,
+                           int training, int accumulate, hipStream_t s) {
+  Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  const int es = p.es, bf = c.bf();
+  const int n = (int)p.chain.size();
+  const std::vector<ChainAct> in = chain_inputs(p, c.sv, nullptr);
+  // an eval-mode forward prepared only the forward weight images
+  if (!training && !p.prep_bwd.empty())
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(), s))
+      return e;
+  int cur = 0;
+  if (int e = c.alloc(cur)) return e;
+  tag(std::string("chain"), "bwd");
+  if (int e = launch_to_cl(dout, c.buf(cur), p.B, p.outd.C, p.outd.Cs, p.outd.vox() / p.B, s, bf, HCU_F32))
+    return e;
+  bool pre = false;   // buf(cur) already holds d(pre-BatchNorm y) of op i
+  for (int i = n - 1; i >= 0; --i) {
+    const ChainOp &o = p.chain[i];
+    const ChainAct &a = in[i];
+    const bool need_dA = i > 0 || dx != nullptr;
+    const ChainOp *pr = i > 0 ? &p.chain[i - 1] : nullptr;
+    if (o.kind == HCU_CHAIN_CONV) {
+      const ConvLayer &L = o.conv;
+      if (o.bn_relu && !pre)
+        if (int e = bn_backward(c, L, c.buf(cur), nullptr, nullptr, training, accumulate)) return e;
+      int sa = -1;
+      float *dA = nullptr;
+      if (need_dA) {
+        if (!L.has_dgrad) return fail(HCU_ERR_UNSUPPORTED, "input gradient of a strided Conv3d");
+        if (int e = c.alloc(sa)) return e;
+        dA = c.buf(sa);
+      }
+      bool done = false;
+      if (L.s2b) {
+        float *dys = c.fptr(c.sc, p.sub_off[1]), *dxs = c.fptr(c.sc, p.sub_off[2]);
+        const int sd[3] = {L.sub_in.X, L.sub_in.Y, L.sub_in.Z}, so[3] = {L.sub_out.X, L.sub_out.Y, L.sub_out.Z};
+        tag(L.name, "wgrad");
+        if (int e = launch_s2b(c.buf(cur), nullptr, nullptr, dys, p.B, L.out.X, L.out.Y, L.out.Z, L.out.Cs, es,
+                               L.L3, so, s))
+          return e;
+        if (int e = conv_backward(c, L, c.fptr(c.sv, o.xs_off), nullptr, nullptr, dys, cur,
+                                  need_dA ? dxs : nullptr, accumulate))
+          return e;
+        if (need_dA)
+          if (int e = launch_b2s(dxs, dA, p.B, L.in.X, L.in.Y, L.in.Z, L.in.Cs, es, L.L3, sd, s)) return e;
+      } else {
+        const ConvLayer *bnl = (pr && pr->kind == HCU_CHAIN_CONV && pr->bn_relu) ? &pr->conv : nullptr;
+        if (int e = conv_backward(c, L, a.x, a.sc, a.sh, c.buf(cur), cur, dA, accumulate, bnl, training, &done))
+          return e;
+      }
+      if (!need_dA) continue;
+      if (i == 0) {
+        if (int e = launch_from_cl(dA, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf)) return e;
+      } else {
+        cur = sa;
+        pre = done;
+      }
+    } else if (o.kind == HCU_CHAIN_POOL) {
+      const ConvLayer &P = pr->conv;
+      int sp = 0;
+      if (int e = c.alloc(sp)) return e;
+      if (int e = bn_backward(c, P, c.buf(sp), c.buf(cur), o.pk, training, accumulate)) return e;
+      cur = sp;
+      pre = true;
+    } else {
+      const ConvTLayer &u = o.ct;
+      float *dU = c.buf(cur);
+      tag(u.name, "wgrad");
+      if (u.b_off >= 0) {
+        const int R = chansum_rows(u.out.vox(), u.out.Cs);
+        float *cs = nullptr;
+        if (int e = c.slab((size_t)R * u.out.Cs, cs)) return e;
+        if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, cs, R, s, bf)) return e;
+        WGradFinalize fb{};
+        fb.partial = cs;
+        fb.db = c.G + u.b_off;
+        fb.KB = R;
+        fb.Mtot = 1;
+        fb.Ntot = u.out.Cs;
+        fb.mode = 2;
+        fb.Cout = u.Cout;
+        fb.accumulate = accumulate;
+        if (int e = c.pend_wgf(fb)) return e;
+      }
+      {
+        WGradArgs w = u.wg;
+        w.A = a.x;
+        w.a_scale = a.sc;
+        w.a_shift = a.sh;
+        w.G = dU;
+        if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
+        if (int e = launch_wgrad(w, s)) return e;
+        WGradFinalize f{};
+        f.partial = w.partial;
+        f.dw = c.G + u.w_off;
+        f.KB = w.KB;
+        f.Mtot = w.Mtot;
+        f.Ntot = w.Ntot;
+        f.T = u.T;
+        f.mode = 1;
+        f.Cin = u.Cin;
+        f.CoutT = u.Cout;
+        f.GCs = w.GCs;
+        f.accumulate = accumulate;
+        if (int e = c.pend_wgf(f)) return e;
+      }
+      if (!need_dA) continue;
+      tag(u.name, "dgrad");
+      int sd = 0;
+      if (int e = c.alloc(sd)) return e;
+      float *dP = c.buf(sd);
+      GConvArgs g = u.dgrad;
+      g.in = dU;
+      g.w = c.fptr(c.sv, u.wd_off);
+      g.out = dP;
+      g.partial = c.kpart();
+      const ConvLayer *bnl = (pr && pr->kind == HCU_CHAIN_CONV && pr->bn_relu) ? &pr->conv : nullptr;
+      const bool fused = fuse_bnbwd(c, g, bnl);
+      if (int e = launch_conv_any(g, s)) return e;
+      if (fused)
+        if (int e = finish_bnbwd(c, g, *bnl, dP, training, accumulate)) return e;
+      if (i == 0) {
+        if (int e = launch_from_cl(dP, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf)) return e;
+      } else {
+        cur = sd;
+        pre = fused;
+      }
+    }
+  }
+  tag(std::string("wgrad"), "finalize");
+  if (int e = c.flush_wgf()) return e;
+  if (timing_on()) timing_set_tag("");
+  return HCU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hcu_chain_plan_create(const hcu_chain_spec *spec, int B, int X, int Y, int Z, hcu_unet_plan **out) {
+  if (!spec || !out) return fail(HCU_ERR_INVALID, "null argument");
+  auto *p = new hcu_unet_plan();
+  p->B = B;
+  p->X = X;
+  p->Y = Y;
+  p->Z = Z;
+  const int e = build_chain(*p, *spec);
+  if (e) {
+    delete p;
+    *out = nullptr;
+    return e;
+  }
+  *out = p;
+  return HCU_OK;
+}
+
+int hcu_chain_plan_query(const hcu_unet_plan *p, int64_t *out_shape, int *n_bn, size_t *saved_bytes,
+                         size_t *scratch_bytes) {
+  if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
+  if (out_shape) {
+    out_shape[0] = p->B;
+    out_shape[1] = p->outd.C;
+    out_shape[2] = p->outd.X;
+    out_shape[3] = p->outd.Y;
+    out_shape[4] = p->outd.Z;
+  }
+  if (n_bn) *n_bn = p->n_bn;
+  if (saved_bytes) *saved_bytes = p->saved_bytes;
+  if (scratch_bytes) *scratch_bytes = p->scratch_bytes;
+  return HCU_OK;
+}
+
+int hcu_chain_forward(const hcu_unet_plan *p, const hcu_unet_tensors *t, int training, hcu_stream_t stream) {
+  if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
+  if (!t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
+    return fail(HCU_ERR_INVALID, "null argument");
+  if (t->x_dtype != HCU_F32 && t->x_dtype != HCU_F16 && !(t->x_dtype == HCU_BF16 && p->es == 2))
+    return fail(HCU_ERR_INVALID, "unsupported input dtype for this plan");
+  if (training)
+    for (const ChainOp &o : p->chain)
+      if (o.kind == HCU_CHAIN_CONV && o.bn_relu && o.conv.bn.count <= 1.0)
+        return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
+  if (p->n_bn && (!t->bn_running_mean || !t->bn_running_var))
+    return fail(HCU_ERR_INVALID, "BatchNorm running statistics missing");
+  return enqueue_chain_forward(*p, t, training, (hipStream_t)stream);
+}
+
+int hcu_chain_backward(const hcu_unet_plan *p, const hcu_unet_tensors *t, const float *dout, float *dx,
+                       int training, int accumulate, hcu_stream_t stream) {
+  if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
+  if (!t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)
+    return fail(HCU_ERR_INVALID, "null argument");
+  return enqueue_chain_backward(*p, t, dout, dx, training, accumulate, (hipStream_t)stream);
 }
 
 }  // extern "C"

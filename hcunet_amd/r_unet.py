@@ -1,0 +1,404 @@
+"""Drop-in hcat.r_unet (RecursiveUnet, RDCNet, f, Down, Up, StackedDilation,
+RDCBlock, crop) whose arithmetic runs in libhcunet.so.
+
+Interface parity with the reference (hcat/r_unet.py):
+  * constructor signatures, module tree and registration order (so
+    state_dict keys and torch's seeded default initialisation match
+    key-for-key and bit-for-bit), save / load (:164-204);
+  * forward semantics, including the 10-step recurrences (:135-162,
+    :219-227), the hard-coded 5-channel / batch-1 state of RecursiveUnet
+    (:141) and the ReLU'd, cat(U, U) decoder blocks (:330-336).
+
+Compute: every Conv3d [+ BatchNorm3d + ReLU] / MaxPool3d / ConvTranspose3d
+sequence between two recurrence points is ONE layer chain
+(hcunet_amd.chain, hcu_chain_* in include/hcunet.h); the gated update of
+RecursiveUnet is a native kernel (hcu_gate_fwd / hcu_gate_bwd).  What is
+left in torch is data movement on the recurrence: the channel cat of the
+input and the state, and RDCNet's residual add.  StackedDilation's dilated
+5^3 convolutions whose halo does not fit a workgroup run on their dilation
+sub-lattices (space-to-batch, hcunet_amd/csrc/layout.hip).  Under
+torch.autocast('cuda', torch.bfloat16) (or compute_dtype = torch.bfloat16)
+the chains run on the bf16 path; RDCNet's last ConvTranspose3d (5 output
+channels: no bf16 phase-folded tiling) stays fp32.
+"""
+import ctypes
+import glob
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .chain import Chain, bf16_active, flat_of, upsample_cat_check
+
+
+def crop(x, y):
+    """hcat/r_unet.py:14-35: x sliced to y's spatial extent (views only)."""
+    assert x.shape[1] == y.shape[1], \
+        f'Inputs do not have same number of feature dimmensions: {x.shape} | {y.shape}'
+    if x.dim() == 4:
+        return x[:, :, 0:y.shape[2]:1, 0:y.shape[3]:1]
+    if x.dim() == 5:
+        return x[:, :, 0:y.shape[2]:1, 0:y.shape[3]:1, 0:y.shape[4]:1]
+    return torch.empty(0)
+
+
+def _chain(owner, root, name, in_channels, ops):
+    """The chain `name` of `owner` over the flat parameters of `root`."""
+    cache = owner.__dict__.setdefault('_hcu_chains', {})
+    key = (id(root), name)
+    ch = cache.get(key)
+    if ch is None or ch.flat.root is not root:
+        ch = Chain(flat_of(root), in_channels, ops)
+        cache[key] = ch
+    return ch
+
+
+def _t3(v):
+    return (v, v, v) if isinstance(v, int) else tuple(v)
+
+
+def _pool_k(mp):
+    k = _t3(mp.kernel_size)
+    s = _t3(mp.stride if mp.stride is not None else mp.kernel_size)
+    if s != k or _t3(mp.padding) != (0, 0, 0) or _t3(mp.dilation) != (1, 1, 1) or mp.ceil_mode:
+        raise NotImplementedError('MaxPool3d must be kernel == stride, no padding, floor mode')
+    return k
+
+
+def _convt_out(ct, shape):
+    k, s, p = _t3(ct.kernel_size), _t3(ct.stride), _t3(ct.padding)
+    return [shape[0], ct.out_channels] + [(shape[2 + d] - 1) * s[d] - 2 * p[d] + k[d] for d in range(3)]
+
+
+def _conv_out(cv, shape):
+    k, s, p, d = _t3(cv.kernel_size), _t3(cv.stride), _t3(cv.padding), _t3(cv.dilation)
+    return [shape[0], cv.out_channels] + [(shape[2 + i] + 2 * p[i] - d[i] * (k[i] - 1) - 1) // s[i] + 1
+                                          for i in range(3)]
+
+
+# ---------------------------------------------------------------------------
+class _Gate(torch.autograd.Function):
+    """h_t = h_prev * sigmoid(zp) + (-1 * sigmoid(zp) * tanh(hp)), h_prev None:
+    ones (hcat/r_unet.py:150-155)."""
+
+    @staticmethod
+    def forward(ctx, hp, zp, hprev):
+        hp, zp = hp.contiguous(), zp.contiguous()
+        if hprev is not None:
+            hprev = hprev.contiguous()
+            if hprev.shape != hp.shape:
+                raise RuntimeError('The size of tensor a (%s) must match the size of tensor b (%s)'
+                                   % (list(hprev.shape), list(hp.shape)))
+        if zp.shape != hp.shape:
+            raise RuntimeError('The size of tensor a (%s) must match the size of tensor b (%s)'
+                               % (list(zp.shape), list(hp.shape)))
+        out = torch.empty_like(hp)
+        _lib.check(_lib.lib().hcu_gate_fwd(_lib.ptr(hp), _lib.ptr(zp), _lib.ptr(hprev), _lib.ptr(out),
+                                           hp.numel(), _lib.stream_handle(hp.device)), 'gate')
+        ctx.has_prev = hprev is not None
+        ctx.save_for_backward(hp, zp, hprev if hprev is not None else hp)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout):
+        hp, zp, hprev = ctx.saved_tensors
+        if not ctx.has_prev:
+            hprev = None
+        dout = dout.contiguous().float()
+        dhp, dzp = torch.empty_like(hp), torch.empty_like(zp)
+        dprev = torch.empty_like(hp) if (hprev is not None and ctx.needs_input_grad[2]) else None
+        _lib.check(_lib.lib().hcu_gate_bwd(_lib.ptr(hp), _lib.ptr(zp), _lib.ptr(hprev), _lib.ptr(dout),
+                                           _lib.ptr(dhp), _lib.ptr(dzp), _lib.ptr(dprev), hp.numel(),
+                                           _lib.stream_handle(hp.device)), 'gate backward')
+        return dhp, dzp, dprev
+
+
+def _ready(x, what):
+    if not isinstance(x, torch.Tensor):
+        raise TypeError('%s must be a torch.Tensor, got %s' % (what, type(x)))
+    _lib.require_device(x, what)
+
+
+# ---------------------------------------------------------------------------
+class Down(nn.Module):
+    """hcat/r_unet.py:249-283: conv1 (padding) -> BN -> ReLU -> conv2
+    (padding 1) -> BN -> ReLU."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel: dict, dilation: dict, groups: dict,
+                 padding=None):
+        super().__init__()
+        if padding is None:
+            padding = 0
+        self.conv1 = nn.Conv3d(in_channels, out_channels, kernel['conv1'], dilation=dilation['conv1'],
+                               groups=groups['conv1'], padding=padding)
+        self.conv2 = nn.Conv3d(out_channels, out_channels, kernel['conv2'], dilation=dilation['conv2'],
+                               groups=groups['conv2'], padding=1)
+        self.batch1 = nn.BatchNorm3d(out_channels)
+        self.batch2 = nn.BatchNorm3d(out_channels)
+        self.relu = nn.ReLU(inplace=True)
+
+    def _ops(self):
+        return [('conv', self.conv1, self.batch1, False), ('conv', self.conv2, self.batch2, False)]
+
+    def out_shape(self, shape):
+        return _conv_out(self.conv2, _conv_out(self.conv1, shape))
+
+    def forward(self, x):
+        _ready(x, 'Down input')
+        return _chain(self, self, 'down', self.conv1.in_channels, self._ops())(
+            x, self.training, bf16_active())
+
+
+class Up(nn.Module):
+    """hcat/r_unet.py:286-336: up_conv (ConvTranspose3d, padding_up) ->
+    cat(U, crop(U, y)) -> conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel: tuple, upsample_kernel: tuple,
+                 upsample_stride: int, dilation: dict, groups: dict, padding_down=None, padding_up=None):
+        super().__init__()
+        if padding_down is None:
+            padding_down = 0
+        if padding_up is None:
+            padding_up = 0
+        self.conv1 = nn.Conv3d(in_channels, out_channels, kernel['conv1'], dilation=dilation['conv1'],
+                               groups=groups['conv1'], padding=padding_down)
+        self.conv2 = nn.Conv3d(out_channels, out_channels, kernel['conv2'], dilation=dilation['conv2'],
+                               groups=groups['conv2'], padding=padding_down)
+        self.up_conv = nn.ConvTranspose3d(in_channels, out_channels, upsample_kernel, stride=upsample_stride,
+                                          padding=padding_up)
+        self.lin_up = False
+        self.batch1 = nn.BatchNorm3d(out_channels)
+        self.batch2 = nn.BatchNorm3d(out_channels)
+        self.relu = nn.ReLU(inplace=True)
+
+    def _ops(self):
+        return [('convt', self.up_conv), ('conv', self.conv1, self.batch1, True),
+                ('conv', self.conv2, self.batch2, False)]
+
+    def check_skip(self, shape, skip_shape):
+        u = _convt_out(self.up_conv, shape)
+        upsample_cat_check(u, torch.empty(skip_shape, device='meta'))
+        return u
+
+    def forward(self, x, y):
+        _ready(x, 'Up input')
+        self.check_skip(list(x.shape), list(y.shape))
+        return _chain(self, self, 'up', self.up_conv.in_channels, self._ops())(
+            x, self.training, bf16_active())
+
+
+class f(nn.Module):
+    """hcat/r_unet.py:232-246: down1 -> max_pool -> down2 -> up1(x, b)."""
+
+    def __init__(self, down1, down2, up1, max_pool):
+        super().__init__()
+        self.down1 = down1
+        self.down2 = down2
+        self.up1 = up1
+        self.max_pool = max_pool
+
+    def _ops(self):
+        return (self.down1._ops() + [('pool', _pool_k(self.max_pool))] + self.down2._ops()
+                + self.up1._ops())
+
+    def _run(self, x, root, training, bf16):
+        b = self.down1.out_shape(list(x.shape))
+        p = [b[0], b[1]] + [b[2 + d] // _pool_k(self.max_pool)[d] for d in range(3)]
+        self.up1.check_skip(self.down2.out_shape(p), b)
+        return _chain(self, root, 'f', self.down1.conv1.in_channels, self._ops())(x, training, bf16)
+
+    def forward(self, x):
+        _ready(x, 'f input')
+        return self._run(x, self, self.training, bf16_active())
+
+
+class RecursiveUnet(nn.Module):
+    """hcat/r_unet.py:38-204."""
+
+    def __init__(self,
+                 image_dimensions=2,
+                 in_channels=4,
+                 out_channels=5,
+                 kernel={'conv1': (3, 3, 3), 'conv2': (3, 3, 3)},
+                 upsample_kernel=(6, 6, 5),
+                 max_pool_kernel=(2, 2, 1),
+                 upsample_stride=(2, 2, 1),
+                 dilation=1,
+                 groups=1,
+                 ):
+        super().__init__()
+        if type(kernel) is tuple:
+            kernel = {'conv1': kernel, 'conv2': kernel}
+        if type(dilation) is int or type(dilation) is tuple:
+            dilation = {'conv1': dilation, 'conv2': dilation}
+        if type(groups) is int or type(groups) is tuple:
+            groups = {'conv1': groups, 'conv2': groups}
+        self.model_specification = {
+            'image_dimensions': image_dimensions,
+            'in_channels': in_channels,
+            'out_channels': out_channels,
+            'kernel': kernel,
+            'upsample_kernel': upsample_kernel,
+            'max_pool_kernel': max_pool_kernel,
+            'upsample_stride': upsample_stride,
+            'dilation': dilation,
+            'groups': groups
+        }
+        channels = [16, 32, 64]
+        # creation order = the reference's RNG stream (:105-127)
+        self.down1 = Down(in_channels=9, out_channels=channels[0], kernel=kernel, dilation=dilation,
+                          groups=groups, padding=1)
+        self.down2_fz = Down(in_channels=channels[0], out_channels=channels[1], kernel=kernel,
+                             dilation=dilation, groups=groups, padding=1)
+        self.down3_fz = Down(in_channels=channels[1], out_channels=channels[2], kernel=kernel,
+                             dilation=dilation, groups=groups, padding=1)
+        self.up1_fz = Up(in_channels=channels[2], out_channels=channels[1], kernel=kernel, dilation=dilation,
+                         groups=groups, upsample_kernel=upsample_kernel, upsample_stride=upsample_stride,
+                         padding_down=1, padding_up=2)
+        self.down2_fh = Down(in_channels=channels[0], out_channels=channels[1], kernel=kernel,
+                             dilation=dilation, groups=groups, padding=1)
+        self.down3_fh = Down(in_channels=channels[1], out_channels=channels[2], kernel=kernel,
+                             dilation=dilation, groups=groups, padding=1)
+        self.up1_fh = Up(in_channels=channels[2], out_channels=channels[1], kernel=kernel, dilation=dilation,
+                         groups=groups, upsample_kernel=upsample_kernel, upsample_stride=upsample_stride,
+                         padding_down=1, padding_up=2)
+        self.up2 = Up(in_channels=channels[1], out_channels=channels[0], kernel=kernel, dilation=dilation,
+                      groups=groups, upsample_kernel=upsample_kernel, upsample_stride=upsample_stride,
+                      padding_down=1, padding_up=2)
+        self.out_conv = nn.Conv3d(channels[0], out_channels, 1)
+        self.tanh = nn.Tanh()
+        self.sigmoid = nn.Sigmoid()
+        self.max_pool = nn.MaxPool3d(max_pool_kernel)
+        self.fz = f(self.down2_fz, self.down3_fz, self.up1_fz, self.max_pool)
+        self.fh = f(self.down2_fh, self.down3_fh, self.up1_fh, self.max_pool)
+        # None: follow torch.autocast; torch.float32 / torch.bfloat16: force
+        self.compute_dtype = None
+
+    def forward(self, image):
+        _ready(image, 'RecursiveUnet input')
+        bf16 = bf16_active(self)
+        tr = self.training
+        mp = _pool_k(self.max_pool)
+        c_down1 = _chain(self, self, 'down1', 9, self.down1._ops() + [('pool', mp)])
+        c_up2 = _chain(self, self, 'up2', self.up2.up_conv.in_channels,
+                       self.up2._ops() + [('conv', self.out_conv, None, False)])
+        x = None
+        for t in range(10):
+            if t == 0:
+                s_t = torch.zeros([1, 5, image.shape[2], image.shape[3], image.shape[4]],
+                                  device=image.device)
+            x = torch.cat((image, s_t), dim=1)
+            a = self.down1.out_shape(list(x.shape))           # a = down1(x) (its shape only is used)
+            x = c_down1(x, tr, bf16)                           # max_pool(down1(x))
+            hp = self.fh._run(x, self, tr, bf16)
+            zp = self.fz._run(x, self, tr, bf16)
+            h_t = _Gate.apply(hp, zp, None if t == 0 else h_t)
+            self.up2.check_skip(list(h_t.shape), a)
+            x = c_up2(h_t, tr, bf16)                           # out_conv(up2(h_t, a))
+            s_t = x
+        return x
+
+    def save(self, filename, hyperparameters=None):
+        model = {'state_dict': self.state_dict(),
+                 'model_specifications': self.model_specification,
+                 'hyperparameters': hyperparameters}
+        python_files = {}
+        files = glob.glob('./**/*.py', recursive=True) + glob.glob('./**/*.ipynb', recursive=True)
+        for fn in files:
+            with open(fn, 'r') as fh:
+                python_files[fn] = fh.read()
+        model['python_files'] = python_files
+        model['tree_structure'] = glob.glob('**/*', recursive=True)
+        torch.save(model, filename)
+        return None
+
+    def load(self, filename, to_cuda=True):
+        device = 'cuda:0' if (torch.cuda.is_available() and to_cuda) else 'cpu'
+        model = torch.load(filename, map_location=device, weights_only=True)
+        self.__init__()          # the reference re-initialises with the defaults (:197)
+        self.load_state_dict(model['state_dict'])
+        self.eval()
+        try:
+            return model['hyperparameters']
+        except KeyError:
+            return None
+
+
+# ---------------------------------------------------------------------------
+class StackedDilation(nn.Module):
+    """hcat/r_unet.py:339-364: five 'same' Conv3d at dilation 1..5, cat, 1x1."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel: tuple):
+        super().__init__()
+        self.conv1 = nn.Conv3d(in_channels, out_channels, kernel_size=kernel, dilation=1, padding=2)
+        self.conv2 = nn.Conv3d(in_channels, out_channels, kernel_size=kernel, dilation=2, padding=4)
+        self.conv3 = nn.Conv3d(in_channels, out_channels, kernel_size=kernel, dilation=3, padding=6)
+        self.conv4 = nn.Conv3d(in_channels, out_channels, kernel_size=kernel, dilation=4, padding=8)
+        self.conv5 = nn.Conv3d(in_channels, out_channels, kernel_size=kernel, dilation=5, padding=10)
+        self.out_conv = nn.Conv3d(out_channels * 5, out_channels, kernel_size=1, padding=0)
+
+    def _run(self, x, root, bf16, tr):
+        # tr: training flag of the call -- no BatchNorm here; a training call
+        # also lays out the input-gradient weight images during the forward
+        cin = self.conv1.in_channels
+        xs = [_chain(self, root, 'd%d' % i, cin, [('conv', c, None, False)])(x, tr, bf16)
+              for i, c in enumerate((self.conv1, self.conv2, self.conv3, self.conv4, self.conv5))]
+        out = torch.cat(xs, dim=1)
+        return _chain(self, root, 'out', self.out_conv.in_channels, [('conv', self.out_conv, None, False)])(
+            out, tr, bf16)
+
+    def forward(self, x):
+        _ready(x, 'StackedDilation input')
+        return self._run(x, self, bf16_active(), self.training)
+
+
+class RDCBlock(nn.Module):
+    """hcat/r_unet.py:367-378: 1x1 Conv3d (2C -> C) then StackedDilation."""
+
+    def __init__(self, in_channels):
+        super().__init__()
+        self.conv = nn.Conv3d(in_channels * 2, in_channels, kernel_size=1)
+        self.grouped_conv = StackedDilation(in_channels, in_channels, 5)
+
+    def _run(self, x, root, bf16, tr):
+        x = _chain(self, root, 'conv', self.conv.in_channels, [('conv', self.conv, None, False)])(
+            x, tr, bf16)
+        return self.grouped_conv._run(x, root, bf16, tr)
+
+    def forward(self, x):
+        _ready(x, 'RDCBlock input')
+        return self._run(x, self, bf16_active(), self.training)
+
+
+class RDCNet(nn.Module):
+    """hcat/r_unet.py:207-227: strided Conv3d, ten RDCBlock steps on
+    cat(x, y) with a residual state, Conv3d, padded ConvTranspose3d."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        complexity = 10
+        self.strided_conv = nn.Conv3d(in_channels, complexity, kernel_size=3, stride=2, padding=1)
+        self.RDCblock = RDCBlock(complexity)
+        self.out_conv = nn.Conv3d(complexity, out_channels=complexity, kernel_size=3, padding=1)
+        self.transposed_conv = nn.ConvTranspose3d(in_channels=complexity, out_channels=out_channels,
+                                                  stride=(2, 2, 2), kernel_size=(4, 4, 4), padding=(1, 1, 1))
+        self.compute_dtype = None
+
+    def forward(self, x):
+        _ready(x, 'RDCNet input')
+        bf16 = bf16_active(self)
+        tr = self.training
+        x = _chain(self, self, 'strided', self.strided_conv.in_channels,
+                   [('conv', self.strided_conv, None, False)])(x, tr, bf16)
+        y = None
+        for t in range(10):
+            if t == 0:
+                y = torch.zeros(x.shape, device=x.device)
+            in_ = torch.cat((x, y), dim=1)
+            y = self.RDCblock._run(in_, self, bf16, tr) + y
+        y = _chain(self, self, 'out', self.out_conv.in_channels, [('conv', self.out_conv, None, False)])(
+            y, tr, bf16)
+        # 5 output channels: no bf16 phase-folded ConvTranspose3d tiling; fp32
+        return _chain(self, self, 'convt', self.transposed_conv.in_channels,
+                      [('convt', self.transposed_conv)])(y, tr, False)

@@ -214,8 +214,16 @@ class Down(nn.Module):
         self.relu = nn.ReLU(inplace=True)
 
     def forward(self, x):
-        raise NotImplementedError(
-            'Down blocks run inside Unet_Constructor.forward (one fused native call)')
+        """hcat/unet.py:263-266 as one layer chain (hcunet_amd.chain):
+        conv1 -> BN -> ReLU -> conv2 -> BN -> ReLU."""
+        _lib.require_device(x, 'Down input')
+        from .chain import Chain, bf16_active, flat_of
+        ch = self.__dict__.get('_hcu_chain')
+        if ch is None:
+            ch = Chain(flat_of(self), self.conv1.in_channels,
+                       [('conv', self.conv1, self.batch1, False), ('conv', self.conv2, self.batch2, False)])
+            self.__dict__['_hcu_chain'] = ch
+        return ch(x, self.training, bf16_active())
 
 
 class Up(nn.Module):
@@ -246,8 +254,23 @@ class Up(nn.Module):
         self.relu = nn.ReLU(inplace=True)
 
     def forward(self, x, y):
-        raise NotImplementedError(
-            'Up blocks run inside Unet_Constructor.forward (one fused native call)')
+        """hcat/unet.py:309-315 as one layer chain (hcunet_amd.chain):
+        up_conv -> cat(U, crop(U, y)) = cat(U, U) -> conv1 -> BN -> ReLU ->
+        conv2 -> BN -> ReLU."""
+        _lib.require_device(x, 'Up input')
+        from .chain import Chain, bf16_active, flat_of, upsample_cat_check
+        k, st, pd = (_triple(self.up_conv.kernel_size), _triple(self.up_conv.stride),
+                     _triple(self.up_conv.padding))
+        u = [x.shape[0], self.up_conv.out_channels] + [(x.shape[2 + d] - 1) * st[d] - 2 * pd[d] + k[d]
+                                                       for d in range(3)]
+        upsample_cat_check(u, y)
+        ch = self.__dict__.get('_hcu_chain')
+        if ch is None:
+            ch = Chain(flat_of(self), self.up_conv.in_channels,
+                       [('convt', self.up_conv), ('conv', self.conv1, self.batch1, True),
+                        ('conv', self.conv2, self.batch2, False)])
+            self.__dict__['_hcu_chain'] = ch
+        return ch(x, self.training, bf16_active())
 
 
 def crop(x, y):

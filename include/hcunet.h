@@ -167,6 +167,64 @@ typedef struct hcu_bn_layer_info {
 int hcu_unet_plan_bn_layers(const hcu_unet_plan *plan, hcu_bn_layer_info *out, int max);
 
 /* ------------------------------------------------------------------------ */
+/* Layer chains: a short sequence of Conv3d [+ BatchNorm3d + ReLU] /         */
+/* MaxPool3d / ConvTranspose3d [+ cat(U, U)] ops run by the same kernels and */
+/* fusions as the network executor, as one autograd node.  Replaces:         */
+/*   Down.forward / Up.forward of hcat/unet.py:263-266, 309-315 called on    */
+/*   their own, and the layers of hcat/r_unet.py: its Down / Up (padding,    */
+/*   :249-336), f (:232-246), RDCNet's strided / 1x1 / padded ConvTranspose3d */
+/*   (:207-227) and StackedDilation's dilated 5^3 convolutions (:339-364).   */
+/* Input / output tensors are NCXYZ fp32 (the output with the last op's      */
+/* BatchNorm + ReLU applied); parameters / gradients live in flat fp32       */
+/* buffers at the per-op offsets; BatchNorm running statistics are passed    */
+/* per BatchNorm op (hcu_unet_tensors' arrays, in op order).  Plans are      */
+/* hcu_unet_plan objects (hcu_unet_plan_destroy frees them).                 */
+/* ------------------------------------------------------------------------ */
+enum { HCU_CHAIN_CONV = 0, HCU_CHAIN_POOL = 1, HCU_CHAIN_CONVT = 2 };
+#define HCU_CHAIN_MAX_OPS 16
+typedef struct hcu_chain_op {
+  int kind;                  /* HCU_CHAIN_*                                   */
+  int out_channels;          /* CONV / CONVT                                  */
+  int k[3], stride[3], dil[3], pad[3];   /* CONV; CONVT: k, stride, pad (crop) */
+  int groups;                /* CONV                                          */
+  int bn_relu;               /* CONV: followed by BatchNorm3d + ReLU          */
+  int cat_fold;              /* CONV right after a CONVT: its input is cat(U, U)
+                                (hcat/unet.py:311-312; the weight has 2*C input
+                                channels per group and is folded)              */
+  int64_t w_off, b_off;      /* float offsets of weight / bias (b_off < 0: none) */
+  int64_t gamma_off, beta_off;   /* BatchNorm weight / bias (bn_relu)         */
+} hcu_chain_op;
+typedef struct hcu_chain_spec {
+  int n_ops;
+  int in_channels;
+  hcu_chain_op ops[HCU_CHAIN_MAX_OPS];
+  float bn_eps, bn_momentum;     /* < 0 momentum: cumulative average (None)   */
+  int compute_dtype;             /* HCU_F32 or HCU_BF16 (as hcu_unet_spec)    */
+} hcu_chain_spec;
+/* Fails with HCU_ERR_SHAPE where torch would raise for the input shape, with
+ * HCU_ERR_UNSUPPORTED for op combinations the chain does not run (a MaxPool3d
+ * not fed by Conv3d + BatchNorm3d + ReLU, a strided Conv3d's input gradient). */
+int hcu_chain_plan_create(const hcu_chain_spec *spec, int B, int X, int Y, int Z,
+                          hcu_unet_plan **out);
+int hcu_chain_plan_query(const hcu_unet_plan *plan, int64_t *out_shape, int *n_bn,
+                         size_t *saved_bytes, size_t *scratch_bytes);
+/* t->x, t->out: NCXYZ fp32; t->params / t->grads: flat buffers of the op
+ * offsets; training as hcu_unet_forward. */
+int hcu_chain_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
+                      hcu_stream_t stream);
+int hcu_chain_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, const float *dout,
+                       float *dx, int training, int accumulate, hcu_stream_t stream);
+
+/* The gated recurrence of RecursiveUnet.forward (hcat/r_unet.py:150-155), n
+ * fp32 elements: h = tanh(hp), z = sigmoid(zp), out = h_prev*z + (-1*z*h);
+ * h_prev == NULL means ones (the t == 0 state, :152-153).  The backward writes
+ * d(hp), d(zp) and (nullable) d(h_prev) from d(out). */
+int hcu_gate_fwd(const float *hp, const float *zp, const float *h_prev, float *out, int64_t n,
+                 hcu_stream_t stream);
+int hcu_gate_bwd(const float *hp, const float *zp, const float *h_prev, const float *dout, float *dhp,
+                 float *dzp, float *dh_prev, int64_t n, hcu_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Loss.  Replaces hcat.loss.cross_entropy(pred, mask, pwl, method='pixel')  */
 /* hcat/loss.py:5-101: crop mask/pwl top-left to pred (:51-53), BCE with     */
 /* logits * (pwl + 1) computed in pwl's dtype (:65,71-72), mean (:101).      */
