@@ -130,6 +130,7 @@ SYMBOLS = [
     ("hcu_chain_backward", _I, [_VP, ctypes.POINTER(UnetTensors), _VP, _VP, _I, _I, _VP]),
     ("hcu_gate_fwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_gate_bwd", _I, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    ("hcu_gather_vectors", _I, [ctypes.POINTER(_VP), ctypes.POINTER(_I), _I, _VP, _I, _VP]),
     ("hcu_tuning_set_mode", _I, [_I]),
     ("hcu_tuning_get_mode", _I, []),
     ("hcu_tuning_entries", _I64, [ctypes.POINTER(_I64)]),

@@ -697,6 +697,11 @@ int launch_crop_cl(const float *src, float *dst, int B, const int *sdims, const 
                    int Cs, int es, hipStream_t s);
 int launch_from_cl_act(const float *y, const float *sc, const float *sh, float *out, int B, int C, int Cs,
                        int64_t V, hipStream_t s, int bf);
+// LDS-tiled NCXYZ <-> channels-last (Cs <= 128; returns -1 otherwise)
+int launch_from_cl_tiled(const float *y, const float *sc, const float *sh, float *out, int B, int C, int Cs,
+                         int64_t V, hipStream_t s, int bf);
+int launch_to_cl_tiled(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s, int bf,
+                       int x_dtype);
 
 // Loss / optimizer (loss_adam.hip)
 int launch_loss_pixel(const float *pred, int B, int C, int PX, int PY, int PZ,

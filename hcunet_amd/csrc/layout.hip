@@ -11,6 +11,8 @@
 #include "common.h"
 #include "timing.h"
 
+#include <type_traits>
+
 namespace hcu {
 
 int layout_grid(int64_t n) {
@@ -145,8 +147,124 @@ int launch_crop_cl(const float *src, float *dst, int B, const int *sdims, const 
   return 0;
 }
 
+// NCXYZ <-> channels-last through an LDS tile of 64 voxels x Cs channels:
+// the channels-last side moves as contiguous 16-byte vectors, the NCXYZ side
+// as 64 consecutive voxels of one channel (256-byte fp32 rows).  One
+// workgroup per 64-voxel tile (grid.x tiles, grid.y batch).
+constexpr int kTileV = 64;
+template <bool BF>
+__global__ void __launch_bounds__(256)
+from_cl_tile_kernel(const void *y, const float *sc, const float *sh, float *out, int C, int Cs, int64_t V) {
+  extern __shared__ float tl[];   // [kTileV][Cs + 1]
+  const int tid = threadIdx.x;
+  const int64_t v0 = (int64_t)blockIdx.x * kTileV;
+  const int b = blockIdx.y;
+  const int nv = (int)min((int64_t)kTileV, V - v0);
+  const int es = BF ? 2 : 4, per = 16 / es, nvec = Cs / per;
+  const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(y) +
+                                                     ((size_t)b * V + v0) * Cs * es);
+  for (int i = tid; i < nv * nvec; i += 256) {
+    const int v = i / nvec, cv = i % nvec;
+    const uint4 q = src[i];
+    float f[8];
+    if (BF) {
+      unpack8(q, f);
+    } else {
+      const float4 g = __builtin_bit_cast(float4, q);
+      f[0] = g.x; f[1] = g.y; f[2] = g.z; f[3] = g.w;
+    }
+    for (int j = 0; j < per; ++j) tl[v * (Cs + 1) + cv * per + j] = f[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < C * kTileV; i += 256) {
+    const int c = i / kTileV, v = i % kTileV;
+    if (v >= nv) continue;
+    float f = tl[v * (Cs + 1) + c];
+    if (sc) f = fmaxf(fmaf(f, sc[c], sh[c]), 0.f);
+    out[((size_t)b * C + c) * V + v0 + v] = f;
+  }
+}
+
+// x_dtype: 0 fp32, 1 fp16, 3 bf16 input; BF: bf16 channels-last output.
+template <typename TI, bool BF>
+__global__ void __launch_bounds__(256)
+to_cl_tile_kernel(const TI *x, void *xcl, int C, int Cs, int64_t V) {
+  extern __shared__ float tl[];   // [kTileV][Cs + 1]
+  const int tid = threadIdx.x;
+  const int64_t v0 = (int64_t)blockIdx.x * kTileV;
+  const int b = blockIdx.y;
+  const int nv = (int)min((int64_t)kTileV, V - v0);
+  for (int i = tid; i < Cs * kTileV; i += 256) {
+    const int c = i / kTileV, v = i % kTileV;
+    float f = 0.f;
+    if (c < C && v < nv) {
+      const TI w = x[((size_t)b * C + c) * V + v0 + v];
+      if constexpr (sizeof(TI) == 2 && !std::is_same<TI, _Float16>::value)
+        f = bf2f(__builtin_bit_cast(uint16_t, w));
+      else
+        f = (float)w;
+    }
+    tl[v * (Cs + 1) + c] = f;
+  }
+  __syncthreads();
+  const int es = BF ? 2 : 4, per = 16 / es, nvec = Cs / per;
+  uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<char *>(xcl) + ((size_t)b * V + v0) * Cs * es);
+  for (int i = tid; i < nv * nvec; i += 256) {
+    const int v = i / nvec, cv = i % nvec;
+    const float *r = tl + v * (Cs + 1) + cv * per;
+    if (BF) {
+      float f[8];
+      for (int j = 0; j < 8; ++j) f[j] = r[j];
+      dst[i] = pack8(f);
+    } else {
+      dst[i] = __builtin_bit_cast(uint4, make_float4(r[0], r[1], r[2], r[3]));
+    }
+  }
+}
+
+// Tiled layout changes for channel strides up to 128 (else -1: caller falls back).
+int launch_from_cl_tiled(const float *y, const float *sc, const float *sh, float *out, int B, int C, int Cs,
+                         int64_t V, hipStream_t s, int bf) {
+  if (Cs > 128 || B > 65535) return -1;
+  const dim3 grid((unsigned)((V + kTileV - 1) / kTileV), B);
+  const size_t lds = (size_t)kTileV * (Cs + 1) * sizeof(float);
+  const double by = (double)B * V * (C * 4.0 + Cs * (bf ? 2.0 : 4.0));
+  if (bf)
+    HCU_TIMED(s, "from_cl_tile_kernel", 0.0, by,
+              hipLaunchKernelGGL(from_cl_tile_kernel<true>, grid, dim3(256), lds, s, (const void *)y, sc, sh,
+                                 out, C, Cs, V));
+  else
+    HCU_TIMED(s, "from_cl_tile_kernel", 0.0, by,
+              hipLaunchKernelGGL(from_cl_tile_kernel<false>, grid, dim3(256), lds, s, (const void *)y, sc, sh,
+                                 out, C, Cs, V));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+int launch_to_cl_tiled(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hipStream_t s, int bf,
+                       int x_dtype) {
+  if (Cs > 128 || B > 65535) return -1;
+  const dim3 grid((unsigned)((V + kTileV - 1) / kTileV), B);
+  const size_t lds = (size_t)kTileV * (Cs + 1) * sizeof(float);
+  const double by = (double)B * V * (C * (x_dtype == 0 ? 4.0 : 2.0) + Cs * (bf ? 2.0 : 4.0));
+#define TOCL(TI_, BF_)                                                                                    \
+  HCU_TIMED(s, "to_cl_tile_kernel", 0.0, by,                                                             \
+            hipLaunchKernelGGL((to_cl_tile_kernel<TI_, BF_>), grid, dim3(256), lds, s, (const TI_ *)x,     \
+                               (void *)xcl, C, Cs, V))
+  if (x_dtype == 0 && bf) TOCL(float, true);
+  else if (x_dtype == 0) TOCL(float, false);
+  else if (x_dtype == 1 && bf) TOCL(_Float16, true);
+  else if (x_dtype == 1) TOCL(_Float16, false);
+  else if (x_dtype == 3 && bf) TOCL(uint16_t, true);
+  else return -1;
+#undef TOCL
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
 int launch_from_cl_act(const float *y, const float *sc, const float *sh, float *out, int B, int C, int Cs,
                        int64_t V, hipStream_t s, int bf) {
+  if (launch_from_cl_tiled(y, sc, sh, out, B, C, Cs, V, s, bf) == 0) return 0;
   const int64_t n = (int64_t)B * C * V;
   if (bf)
     HCU_TIMED(s, "from_cl_act_kernel", 0.0, 6.0 * n,
@@ -213,3 +331,45 @@ int hcu_gate_bwd(const float *hp, const float *zp, const float *hprev, const flo
   return 0;
 }
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// The BatchNorm running statistics in and out of the data-parallel
+// communication buffer (hcunet_amd/dist.py): n small vectors gathered into /
+// scattered from one contiguous buffer in one launch (one workgroup each).
+namespace hcu {
+constexpr int kVecMax = 128;
+struct VecList {
+  float *p[kVecMax];
+  int off[kVecMax + 1];
+  int n, unpack;
+};
+__global__ void __launch_bounds__(256) vec_gather_kernel(const VecList v, float *buf) {
+  const int j = blockIdx.x;
+  float *p = v.p[j];
+  const int o = v.off[j], len = v.off[j + 1] - o;
+  for (int i = threadIdx.x; i < len; i += 256) {
+    if (v.unpack) p[i] = buf[o + i];
+    else buf[o + i] = p[i];
+  }
+}
+}  // namespace hcu
+
+extern "C" int hcu_gather_vectors(float *const *vecs, const int *lens, int n, float *buf, int unpack,
+                                  void *stream) {
+  if (n < 0 || n > hcu::kVecMax || (n && (!vecs || !lens || !buf)))
+    return hcu::fail(1, "hcu_gather_vectors: 0..128 vectors");
+  if (n == 0) return 0;
+  hcu::VecList v{};
+  v.off[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    v.p[i] = vecs[i];
+    v.off[i + 1] = v.off[i] + lens[i];
+  }
+  v.n = n;
+  v.unpack = unpack != 0;
+  hipStream_t s = (hipStream_t)stream;
+  HCU_TIMED(s, "vec_gather_kernel", 0.0, 8.0 * v.off[n],
+            hipLaunchKernelGGL(hcu::vec_gather_kernel, dim3(n), dim3(256), 0, s, v, buf));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}

@@ -1187,6 +1187,7 @@ int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hi
     HCU_CHECK_LAUNCH();
     return 0;
   }
+  if (launch_to_cl_tiled(x, xcl, B, C, Cs, V, s, bf, x_dtype) == 0) return 0;
   if (x_dtype == 1 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
               hipLaunchKernelGGL((to_cl_kernel<_Float16, bf16_t>), gr, dim3(256), 0, s,
@@ -1229,6 +1230,7 @@ from_cl_kernel(const T *xcl, float *x, int B, int C, int Cs, int64_t V) {
 
 int launch_from_cl(const float *xcl, float *x, int B, int C, int Cs, int64_t V, hipStream_t s,
                    int bf) {
+  if (launch_from_cl_tiled(xcl, nullptr, nullptr, x, B, C, Cs, V, s, bf) == 0) return 0;
   const int64_t n = (int64_t)B * C * V;
   HCU_TIMED(s, "from_cl_kernel", 0.0, 0.0,
             HCU_BF_DISPATCH(bf, from_cl_kernel, dim3(grid_for(n)), dim3(256), 0, s,

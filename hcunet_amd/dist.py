@@ -63,10 +63,13 @@ def allreduce_gradients(module, group=None, bn_stats=True):
             off += p.numel()
         flat_ok = flat_ok and off == G.numel() and C.data_ptr() == base \
             and C.numel() >= G.numel() + nstat
+    native = flat_ok and C.is_cuda and 0 < len(stats) <= 128 and all(t.is_contiguous() for t in stats)
     if flat_ok:
         buf = C[:G.numel() + nstat]
         tail = buf[G.numel():]
-        if stats:
+        if native:
+            _stats_move(stats, tail, unpack=False)   # one launch
+        elif stats:
             torch.cat([t.reshape(-1) for t in stats], out=tail)
     else:
         buf = torch.cat([p.grad.reshape(-1) for p in params] + [t.reshape(-1) for t in stats])
@@ -81,10 +84,26 @@ def allreduce_gradients(module, group=None, bn_stats=True):
             k = p.numel()
             p.grad.copy_(buf[off:off + k].view_as(p.grad))
             off += k
+    if native:
+        _stats_move(stats, buf[off:], unpack=True)   # one launch
+        return
     for t in stats:
         k = t.numel()
         t.copy_(buf[off:off + k].view_as(t))
         off += k
+
+
+def _stats_move(stats, buf, unpack):
+    """The running statistics into (unpack=False) / out of the communication
+    buffer's tail in ONE launch (hcu_gather_vectors)."""
+    import ctypes
+    from . import _lib
+    n = len(stats)
+    ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in stats])
+    lens = (ctypes.c_int * n)(*[t.numel() for t in stats])
+    _lib.check(_lib.lib().hcu_gather_vectors(ptrs, lens, n, ctypes.c_void_p(buf.data_ptr()),
+                                             1 if unpack else 0, _lib.stream_handle(buf.device)),
+               'allreduce_gradients')
 
 
 def deterministic_tiling():

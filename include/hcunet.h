@@ -224,6 +224,12 @@ int hcu_gate_fwd(const float *hp, const float *zp, const float *h_prev, float *o
 int hcu_gate_bwd(const float *hp, const float *zp, const float *h_prev, const float *dout, float *dhp,
                  float *dzp, float *dh_prev, int64_t n, hcu_stream_t stream);
 
+/* Data parallel (hcunet_amd/dist.py): n <= 128 fp32 vectors (the BatchNorm
+ * running statistics) gathered into (unpack = 0) or scattered from
+ * (unpack = 1) one contiguous buffer in one launch, in order. */
+int hcu_gather_vectors(float *const *vecs, const int *lens, int n, float *buf, int unpack,
+                       hcu_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Loss.  Replaces hcat.loss.cross_entropy(pred, mask, pwl, method='pixel')  */
 /* hcat/loss.py:5-101: crop mask/pwl top-left to pred (:51-53), BCE with     */

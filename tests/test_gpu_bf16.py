@@ -112,3 +112,9 @@ def test_bf16_config3_larger_tile():
 def test_bf16_16bit_volume_input(x_dtype):
     """16-bit confocal volumes go straight into the first kernel (no host cast)."""
     _check(*_run(dict(REF_KW, feature_sizes=[16, 32, 64]), (2, 4, 44, 44, 5), x_dtype=x_dtype))
+
+
+def test_bf16_config3_full_size():
+    """BASELINE config 3 exactly as benched: [32..512], B=4, 256x256x16 (the
+    tilings come from the persistent table, as in bench.py)."""
+    _check(*_run(CFG3, (4, 4, 256, 256, 16)))
