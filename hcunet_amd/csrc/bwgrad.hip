@@ -562,7 +562,9 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   // padded operands (zero padding of A, or a cropped ConvTranspose3d output
   // as G) are staged as zeros outside their grids
   // channel chunks: A side up to 32 channels, G side up to 64 (16-col subtiles)
-  a.CKA = std::min(a.ACs, 32);
+  // (HCU_BW_CKA caps the A chunk: experiments)
+  const int cka_cap = getenv("HCU_BW_CKA") ? atoi(getenv("HCU_BW_CKA")) : 32;
+  a.CKA = std::min(a.ACs, cka_cap);
   if (a.ACs % a.CKA) a.CKA = 8;
   a.CKG = std::min(a.GCs, 64);
   if (a.GCs % a.CKG) a.CKG = (a.GCs % 32 == 0) ? 32 : (a.GCs % 16 == 0 ? 16 : 8);
@@ -573,7 +575,7 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
     const int rows_all = T * a.CKA;                    // all taps of one channel chunk
     const int sub_all = cdiv(rows_all, 16);
     int msw = cdiv(sub_all, 4);
-    if (msw > 9) msw = 5;                              // split the taps over blocks
+    if (msw > 9) msw = 9;                              // split the taps over blocks (36 rows each)
     a.MSW = msw <= 3 ? 3 : (msw <= 5 ? 5 : 9);
     a.TA = std::min(T, (a.MSW * 4 * 16) / a.CKA);
     if (a.TA < 1) return fail(4, "bwgrad: channel chunk too large");
@@ -608,7 +610,8 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   a.PG2 = a.CKG + 8;
   const int txys[3][2] = {{8, 8}, {4, 8}, {4, 8}};
   long lds = 0;
-  for (int i = 0; i < 3; ++i) {
+  const int t0i = getenv("HCU_BW_TILE") ? std::max(0, std::min(2, atoi(getenv("HCU_BW_TILE")))) : 0;
+  for (int i = t0i; i < 3; ++i) {
     a.TX = txys[i][0];
     a.TY = txys[i][1];
     a.HAX = (a.TX - 1) * a.asx + (a.taps_rows ? (a.KX - 1) * a.adx : 0) + 1;
@@ -646,7 +649,8 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   // One fp32 slab per block: the pipelined kernel hides its loads behind the
   // MFMAs of the same block, so it needs at most two blocks per CU -- fewer
   // blocks, fewer slabs for the finalize to read.
-  const int occ_kb = a.NPA ? std::min(a.occ, 2) : a.occ;
+  const int occ_cap = getenv("HCU_BW_OCC") ? std::max(1, atoi(getenv("HCU_BW_OCC"))) : 2;
+  const int occ_kb = a.NPA ? std::min(a.occ, occ_cap) : a.occ;
   long kb = std::max(1L, (long)256 * occ_kb / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;

@@ -39,9 +39,12 @@ def import_runet():
     return runet, unet, loss
 
 
-def run(net, loss_mod, x, mask, pwl, vec, dtype):
-    net = net.to(dtype).train()
+def run(net, loss_mod, x, mask, pwl, vec, dtype, train=True, noise=None):
+    net = net.to(dtype).train(train)
     xx = torch.from_numpy(x).to(dtype)
+    if noise is not None:   # (seed, relative amplitude): sensitivity probe
+        gen = torch.Generator().manual_seed(noise[0])
+        xx = xx * (1 + noise[1] * torch.randn(xx.shape, generator=gen, dtype=dtype))
     net.zero_grad()
     out = net(xx)
     lp = loss_mod.cross_entropy(out[:, 0:1], torch.from_numpy(mask).to(dtype),
@@ -62,7 +65,7 @@ def summary(t):
                            t[torch.from_numpy(idx)].numpy()])
 
 
-def record(name, make, shape, seed, full=True):
+def record(name, make, shape, seed, full=True, eval_too=False, sens=0):
     """full=False: weights and gradients as digests (summary) -- the weights are
     re-created on the GPU side from the same seed (the drop-in modules
     reproduce torch's default initialisation in the reference's order)."""
@@ -91,6 +94,31 @@ def record(name, make, shape, seed, full=True):
             rec[tag + '.grad.' + k] = g.numpy() if full else summary(g)
         for k, b in bufs.items():
             rec[tag + '.buf.' + k] = b.numpy()
+    # eval mode (BatchNorm on the running statistics): the gradients no longer
+    # pass ten steps of batch statistics, so they are not noise-amplified
+    for tag, dt in ((('e32', torch.float32), ('e64', torch.float64)) if eval_too else ()):
+        net = make(runet)
+        net.load_state_dict(state)
+        out, ls, grads, _ = run(net, loss, x, mask, pwl, vec, dt, train=False)
+        rec[tag + '.out'] = out.numpy()
+        rec[tag + '.loss'] = np.array(ls.item())
+        for k, g in grads.items():
+            rec[tag + '.grad.' + k] = g.numpy() if full else summary(g)
+    # sensitivity envelope of the train-mode gradients: the reference's own
+    # fp32 run with the input perturbed by 1e-6 relative noise (the size of a
+    # reordered fp32 reduction's rounding), `sens` seeds; per tensor the
+    # largest digest relative L2 against the unperturbed fp64 run
+    for k in (grads.keys() if sens else ()):
+        rec['sens.grad.' + k] = np.array(0.0)
+    for s in range(sens):
+        net = make(runet)
+        net.load_state_dict(state)
+        _, _, grads, _ = run(net, loss, x, mask, pwl, vec, torch.float32, noise=(100 + s, 1e-6))
+        for k, g in grads.items():
+            d, d64 = summary(g), rec['f64.grad.' + k]
+            d64 = d64 if not full else summary(torch.from_numpy(d64))
+            r = np.linalg.norm(d - d64) / max(np.linalg.norm(d64), 1e-12)
+            rec['sens.grad.' + k] = np.maximum(rec['sens.grad.' + k], r)
     rec['vec'] = vec
     path = os.path.join(HERE, name + '.npz')
     np.savez_compressed(path, **rec)
@@ -145,5 +173,6 @@ def record_blocks():
 
 if __name__ == '__main__':
     record('runet_rdc', lambda m: m.RDCNet(4, 5), (1, 4, 24, 24, 10), 0)
-    record('runet_rec', lambda m: m.RecursiveUnet(image_dimensions=3), (1, 4, 16, 16, 4), 1, full=False)
+    record('runet_rec', lambda m: m.RecursiveUnet(image_dimensions=3), (1, 4, 16, 16, 4), 1, full=False,
+           eval_too=True, sens=4)
     record_blocks()

@@ -51,6 +51,10 @@ def main():
     ap.add_argument('fetch_dir')
     ap.add_argument('write_dir')
     ap.add_argument('--out', default=None)
+    ap.add_argument('--steps', type=float, default=0,
+                    help='steps the profiled run executed (warm-up included): adds per-step totals')
+    ap.add_argument('--compulsory', type=float, default=0,
+                    help='compulsory HBM bytes per step (SURVEY 8d) to compare with')
     a = ap.parse_args()
     fetch = read_counter(a.fetch_dir, 'FETCH_SIZE')
     write = read_counter(a.write_dir, 'WRITE_SIZE')
@@ -63,6 +67,15 @@ def main():
                   'write_bytes_per_launch': wb, 'hbm_bytes_per_launch': fb + wb}
     tab['_note'] = ('FETCH_SIZE x2 (gfx950 counts half of a wide coalesced read) + WRITE_SIZE, '
                     'KiB -> bytes, averaged over the dispatches of each kernel symbol')
+    if a.steps:
+        per = {k: v['hbm_bytes_per_launch'] * v['launches'] / a.steps for k, v in tab.items()
+               if not k.startswith('_')}
+        tot = sum(per.values())
+        tab['_per_step'] = {'steps': a.steps, 'hbm_bytes': tot, 'compulsory_bytes': a.compulsory or None,
+                            'ratio': tot / a.compulsory if a.compulsory else None,
+                            'by_kernel': dict(sorted(per.items(), key=lambda kv: -kv[1]))}
+        print('per step: %.3f GB (compulsory %.3f GB, ratio %s)' % (
+            tot / 1e9, a.compulsory / 1e9, '%.2f' % (tot / a.compulsory) if a.compulsory else '-'))
     if a.out:
         with open(a.out, 'w') as f:
             json.dump(tab, f, indent=1, sort_keys=True)

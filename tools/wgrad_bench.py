@@ -17,6 +17,9 @@ from hcunet_amd import _lib  # noqa: E402
 from tests.helpers import desc, out_dims, scratch_for, stream  # noqa: E402
 
 SHAPES = {   # name: B, Cin, Cout, X, Y, Z, k
+    'c3.d0.c2': (4, 32, 32, 254, 254, 15, (3, 3, 1)),    # config 3 (bf16 with --bf16)
+    'c3.d1.c2': (4, 64, 64, 125, 125, 13, (3, 3, 1)),
+    'c3.d1.c1': (4, 32, 64, 127, 127, 14, (3, 3, 2)),
     'd0.c1': (2, 4, 8, 256, 256, 16, (3, 3, 2)),
     'd0.c2': (2, 8, 8, 254, 254, 15, (3, 3, 1)),
     'd1.c1': (2, 8, 16, 127, 127, 14, (3, 3, 2)),
@@ -28,16 +31,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--only', default=None)
+    ap.add_argument('--bf16', action='store_true')
     a = ap.parse_args()
     L = _lib.lib()
     for name, (B, Cin, Cout, X, Y, Z, k) in SHAPES.items():
         if a.only and name not in a.only.split(','):
             continue
         d = desc(B, Cin, Cout, X, Y, Z, k)
+        q = 4
+        if a.bf16:
+            d.dtype = _lib.HCU_BF16
+            q = 8
         od = out_dims(d)
-        cs_in, cs_out = (Cin + 3) // 4 * 4, (Cout + 3) // 4 * 4
-        x = torch.randn(B, X, Y, Z, cs_in, device='cuda')
-        gy = torch.randn(B, *od, cs_out, device='cuda')
+        cs_in, cs_out = (Cin + q - 1) // q * q, (Cout + q - 1) // q * q
+        dt = torch.bfloat16 if a.bf16 else torch.float32
+        x = torch.randn(B, X, Y, Z, cs_in, device='cuda').to(dt)
+        gy = torch.randn(B, *od, cs_out, device='cuda').to(dt)
         dw = torch.empty(Cout, Cin, *k, device='cuda')
         db = torch.empty(Cout, device='cuda')
         sc = scratch_for(d)
