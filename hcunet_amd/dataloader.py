@@ -60,6 +60,18 @@ class _Raw:
         return t.PendingVolume(r, np_dtype=self.np_dtype)
 
 
+_LAZY = (t.to_float, t.reshape, t.normalize, t.to_tensor)
+
+
+def _arrays_for(transform, items):
+    """The lazy device chain understands PendingVolume; any other transform
+    (the reference's random augmentations, a caller's own) gets the ndarray
+    the reference's eager chain would hold at that point."""
+    if isinstance(transform, _LAZY):
+        return items
+    return [x.to_ndarray() if isinstance(x, t.PendingVolume) else x for x in items]
+
+
 class Stack(torch.utils.data.Dataset):
     """Dataloader for hcat.unet: 3D stacks with mask and pixel-weight maps."""
 
@@ -99,10 +111,13 @@ class Stack(torch.utils.data.Dataset):
         mask = self.mask[item].pending(expand=True)
         pwl = self.pwl[item].pending(expand=True)
         for jt in self.joint_transforms:
+            image, mask, pwl = _arrays_for(jt, [image, mask, pwl])
             image, mask, pwl = jt([image, mask, pwl])
         for it in self.image_transforms:
+            image = _arrays_for(it, [image])[0]
             image = it(image)
         for ot in self.out_transforms:
+            image, mask, pwl = _arrays_for(ot, [image, mask, pwl])
             image, mask, pwl = ot([image, mask, pwl])
         return image, mask, pwl
 

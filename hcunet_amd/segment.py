@@ -146,6 +146,21 @@ def _slice_len(start, stop, n):
     return a, max(0, b - a)
 
 
+def _tile_bytes(unet, C, tdims):
+    """Device bytes one tile of a batched forward needs: its fp32 input, its
+    output, and the forward's own workspaces (the plan's saved + scratch
+    bytes at batch 1; the workspaces scale with the batch)."""
+    vox = tdims[0] * tdims[1] * tdims[2]
+    eng_fn = getattr(unet, 'engine', None)
+    if eng_fn is None:   # not this package's network: a conservative guess
+        return 4 * C * vox * 64
+    eng = eng_fn()
+    # the driver's forward runs under no_grad: the forward-only plan
+    plan = eng.plan((1, C) + tuple(tdims), unet._bf16(), forward_only=True)
+    out = 4 * plan.out_shape[1] * plan.out_shape[2] * plan.out_shape[3] * plan.out_shape[4]
+    return 4 * C * vox + out + plan.saved_bytes + plan.scratch_bytes
+
+
 def predict_segmentation_mask(unet, image, device=None, use_probability_map=False,
                               mask_cell_prob_threshold=0.5, tiles_per_batch=None,
                               total_memory=None):
@@ -202,12 +217,10 @@ def predict_segmentation_mask(unet, image, device=None, use_probability_map=Fals
                 raise RuntimeError(f'Amount of padding is not sufficient.\nvalid_out.shape: n/a\n'
                                    f'eval_image_size: {ev} ')
             j = i + 1
-            per_tile = 4 * C * tdims[0] * tdims[1] * tdims[2]
             cap = batch_cap
             if tiles_per_batch is None and cap > 1:
                 free = torch.cuda.mem_get_info(dev)[0]
-                # input + ~12 activation-sized buffers per tile (forward-only plan)
-                cap = max(1, min(cap, int(free / 4 // (per_tile * 12))))
+                cap = max(1, min(cap, int(free / 4 // _tile_bytes(unet, C, tdims))))
             while j < len(tiles) and j - i < cap and tiles[j][1] == tdims:
                 j += 1
             batch = tiles[i:j]
@@ -215,7 +228,22 @@ def predict_segmentation_mask(unet, image, device=None, use_probability_map=Fals
             _gather(vol, pads, [t[0] for t in batch], tdims, True, xb, stream)
             # "Occasionally everything is just -1 in the whole mat. Skip for speed"
             skip = (xb == -1).flatten(1).all(1).tolist()
-            out = unet(xb)
+            try:
+                out = unet(xb)
+            except torch.OutOfMemoryError:
+                if len(batch) == 1 or tiles_per_batch is not None:
+                    raise
+                # the estimate was optimistic (fragmentation, other tenants):
+                # retry this run of tiles with half the batch
+                del xb
+                batch_cap = max(1, len(batch) // 2)
+                continue
+            except RuntimeError as e:   # native workspace allocation failures
+                if len(batch) == 1 or tiles_per_batch is not None or 'out of memory' not in str(e):
+                    raise
+                del xb
+                batch_cap = max(1, len(batch) // 2)
+                continue
             if not out.is_contiguous() or out.dtype != torch.float32:
                 out = out.float().contiguous()
             Co, OX, OY, OZ = out.shape[1:]

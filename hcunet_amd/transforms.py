@@ -53,6 +53,36 @@ class PendingVolume:
             s = (s[-2],) + s[1:-2] + (s[0], s[-1])
         return s
 
+    def to_ndarray(self):
+        """The ndarray the reference's eager chain would hold at this point
+        (host numpy, same arithmetic: to_float :104-115, reshape :139-156,
+        normalize :266-281), for transforms that need a real array (the
+        reference's random augmentations check isinstance(image, np.ndarray))."""
+        raw = self.raw
+        if isinstance(raw, torch.Tensor):
+            a = raw.detach().cpu().numpy()
+            if self.np_dtype is not None and np.dtype(self.np_dtype) != a.dtype:
+                a = a.view(self.np_dtype)
+            elif raw.dtype == torch.int16:
+                a = a.view(np.uint16)
+        else:
+            a = np.asarray(raw)
+        if self.to_float:
+            if a.dtype == np.uint16:
+                a = a.astype(np.float64) / 2 ** 16
+            elif a.dtype == np.uint8:
+                a = a.astype(np.float64) / 2 ** 8
+        else:
+            a = a.copy()
+        if self.reshaped:
+            a = a.swapaxes(a.ndim - 2, 0)
+        if self.mean is not None:
+            a = np.ascontiguousarray(a)
+            for c in range(a.shape[-1]):
+                a[..., c] += -self.mean[c]
+                a[..., c] /= self.std[c]
+        return a
+
     def _dtype_code(self):
         if self.np_dtype is not None:
             return _RAW.get(np.dtype(self.np_dtype))

@@ -89,6 +89,29 @@ def test_forward_only_plan_matches_training_plan_output():
     assert p_fwd.scratch_bytes < p_full.scratch_bytes
 
 
+def test_forward_only_plan_train_mode_matches_full_plan():
+    """Train-mode BatchNorm under no_grad (the tiled driver in m.train()) runs
+    the forward-only plan with batch statistics: its output and the updated
+    running mean / var / num_batches_tracked equal one train-mode forward of
+    the full plan (the two plans may pick different convolution tilings, so
+    to fp32 summation-order rounding)."""
+    g = gold()
+    x = torch.from_numpy(np.nan_to_num(golden_volume(g).numpy()[:, :, :96, :96, :])).cuda()
+    ma, mb = _net(g).train(), _net(g).train()
+    nbt0 = [int(b.num_batches_tracked) for b in ma.modules() if isinstance(b, torch.nn.BatchNorm3d)]
+    with torch.no_grad():
+        ya = ma(x)
+    yb = mb(x.clone().requires_grad_(True)).detach()
+    scale = max(yb.abs().max().item(), 1e-6)
+    assert (ya - yb).abs().max().item() <= 1e-5 * scale
+    bns = [(a, b) for a, b in zip(ma.modules(), mb.modules()) if isinstance(a, torch.nn.BatchNorm3d)]
+    for (a, b), n0 in zip(bns, nbt0):
+        assert int(a.num_batches_tracked) == int(b.num_batches_tracked) == n0 + 1
+        for s in ('running_mean', 'running_var'):
+            ra, rb = getattr(a, s), getattr(b, s)
+            assert (ra - rb).abs().max().item() <= 1e-5 * max(rb.abs().max().item(), 1e-6), s
+
+
 def test_train_mode_runs_tile_by_tile():
     """In train mode BatchNorm uses batch statistics, so tiles run one at a
     time (as the reference's loop does) and the running statistics move."""

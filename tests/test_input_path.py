@@ -65,3 +65,40 @@ def test_oracle_to_tensor_rounds_like_torch():
     want = torch.as_tensor(vals, dtype=torch.half).numpy().view(np.uint16)
     np.testing.assert_array_equal(got, want)
     assert np.float16(v).view(np.uint16) != got[0]
+
+
+def test_stack_hands_ndarrays_to_other_transforms(tmp_path):
+    """a transform that is not part of the lazy device chain (the
+    reference's augmentations check isinstance(image, np.ndarray)) receives the
+    array the reference's eager to_float -> reshape -> normalize would hold."""
+    rng = np.random.default_rng(5)
+    raw = rng.integers(0, 65536, (3, 6, 5, 4)).astype(np.uint16)
+    mask = rng.integers(0, 2, (3, 6, 5)).astype(np.uint8)
+    pwl = rng.integers(0, 256, (3, 6, 5)).astype(np.uint8)
+    files = {'a.tif': raw, 'a.mask.tif': mask, 'a.pwl.tif': pwl}
+    for n in files:
+        (tmp_path / n).write_bytes(b'')
+    seen = []
+
+    class probe:
+        def __call__(self, image):
+            assert isinstance(image, np.ndarray)
+            seen.append(image.copy())
+            return image
+
+    def reader(p):
+        return files[os.path.basename(p)]
+
+    ds = Stack(str(tmp_path), [tr.to_float(), tr.reshape(), tr.normalize([0.3] * 4, [0.7] * 4), probe()],
+               [], out_transforms=[], reader=reader)
+    img, m, w = ds[0]
+    want = raw.astype(np.float64) / 2 ** 16
+    want = want.swapaxes(2, 0)
+    for c in range(4):
+        want[..., c] += -0.3
+        want[..., c] /= 0.7
+    np.testing.assert_array_equal(seen[0], want)
+    assert isinstance(img, np.ndarray)
+    # the untouched mask stays lazy (raw bits, channel axis added)
+    assert isinstance(m, tr.PendingVolume) and m.shape == (3, 6, 5, 1)
+    np.testing.assert_array_equal(m.to_ndarray()[..., 0], mask)
