@@ -248,6 +248,37 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
   };
 
+  // ---- weights of a block that walks several channel chunks per tile (the
+  // deep levels: few tiles, K split over chunks inside the block): the next
+  // chunk's packed weights are loaded into registers with the next halo, so
+  // the per-chunk weight staging no longer waits on an L2 round trip.  Up to
+  // WPR 16-byte elements per thread (NT = 16: S <= 20; NT = 32: S <= 10);
+  // larger images keep the synchronous stage_w.
+  constexpr int WPR = 5;
+  const int n16w = S * 4 * NT;
+  const bool wpre = NPF > 0 && nck > 1 && n16w <= 256 * WPR;
+  uint4 wpf[WPR];
+  auto wfetch = [&](int chunk) {
+    const int CoutW = KA(CoutW);
+    const uint32_t nrec = (uint32_t)nchunks * S * 4 * CoutW * 16;
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)KA(w), 0, (int)nrec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < WPR; ++u) {
+      const int idx = tid + u * 256;
+      const int n = idx % NT, sg = idx / NT;
+      const int off = idx < n16w ? (((chunk * S * 4 + sg) * CoutW + (int)blockIdx.y * NT + n) * 16) : 0x7ffffff0;
+      wpf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+    }
+  };
+  auto wstore = [&]() {   // every thread writes WPR slots (past the image: the dummy slot region)
+#pragma unroll
+    for (int u = 0; u < WPR; ++u) {
+      const int idx = tid + u * 256;
+      if (idx < n16w) reinterpret_cast<uint4 *>(wlds)[idx] = wpf[u];
+    }
+  };
+
   // ---- halo staging: thread tid owns 16-byte channel group cv = tid % CV of
   // halo voxels v = tid / CV + u * (256 / CV); their halo coordinates are fixed.
   constexpr int VS = 256 / CV;
@@ -500,7 +531,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   if (NPF > 0) {
     int tile = t_beg;
     if (nck == 1) stage_w(cb);
-    if (tile < t_end) fetch(tile, cb);
+    if (tile < t_end) {
+      fetch(tile, cb);
+      if (wpre) wfetch(cb);
+    }
     dummy_epilogue();
     for (; tile < t_end; ++tile) {
 #pragma unroll
@@ -514,7 +548,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
           *reinterpret_cast<uint4 *>(alds + (hpk[u] >= 0 ? (tid / CV + u * VS) * CKP + cv * VEC : HV * CKP)) =
               activate(pf[u], (okbits >> u) & 1u, chunk);
         PH_MARK(0);
-        if (nck > 1) stage_w(chunk);
+        if (wpre)
+          wstore();
+        else if (nck > 1)
+          stage_w(chunk);
         lds_barrier();
         PH_MARK(1);
         int nt = tile, nc = chunk + 1;
@@ -522,7 +559,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
           nc = cb;
           nt = tile + 1;
         }
-        if (nt < t_end) fetch(nt, nc);
+        if (nt < t_end) {
+          fetch(nt, nc);
+          if (wpre) wfetch(nc);
+        }
         PH_MARK(2);
         compute();
         PH_MARK(3);

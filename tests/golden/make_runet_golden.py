@@ -174,5 +174,5 @@ def record_blocks():
 if __name__ == '__main__':
     record('runet_rdc', lambda m: m.RDCNet(4, 5), (1, 4, 24, 24, 10), 0)
     record('runet_rec', lambda m: m.RecursiveUnet(image_dimensions=3), (1, 4, 16, 16, 4), 1, full=False,
-           eval_too=True, sens=4)
+           eval_too=True, sens=16)
     record_blocks()
