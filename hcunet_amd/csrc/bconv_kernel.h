@@ -253,10 +253,14 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // chunk's packed weights are loaded into registers with the next halo, so
   // the per-chunk weight staging no longer waits on an L2 round trip.  Up to
   // WPR 16-byte elements per thread (NT = 16: S <= 20; NT = 32: S <= 10);
-  // larger images keep the synchronous stage_w.
-  constexpr int WPR = 5;
+  // larger images keep the synchronous stage_w.  Only in the instances whose
+  // register budget has room for the 20 extra VGPRs (NSUB <= 2, NPF <= 8):
+  // measured on MI355X, the NSUB = 4 / NPF = 12 input-gradient variants lost
+  // occupancy and ran 40-60 % slower with them.
+  constexpr bool WPOK = NPF > 0 && NPF <= 8 && NSUB <= 2;
+  constexpr int WPR = WPOK ? 5 : 1;
   const int n16w = S * 4 * NT;
-  const bool wpre = NPF > 0 && nck > 1 && n16w <= 256 * WPR;
+  const bool wpre = WPOK && nck > 1 && n16w <= 256 * WPR;
   uint4 wpf[WPR];
   auto wfetch = [&](int chunk) {
     const int CoutW = KA(CoutW);
