@@ -131,6 +131,10 @@ SYMBOLS = [
     ("hcu_gate_fwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_gate_bwd", _I, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_gather_vectors", _I, [ctypes.POINTER(_VP), ctypes.POINTER(_I), _I, _VP, _I, _VP]),
+    ("hcu_unet_set_grad_events", _I, [_VP, _VP, _VP, _I]),
+    ("hcu_event_create", _I, [ctypes.POINTER(_VP)]),
+    ("hcu_event_destroy", _I, [_VP]),
+    ("hcu_stream_wait_event", _I, [_VP, _VP]),
     ("hcu_tuning_set_mode", _I, [_I]),
     ("hcu_tuning_get_mode", _I, []),
     ("hcu_tuning_entries", _I64, [ctypes.POINTER(_I64)]),

@@ -447,9 +447,15 @@ struct WGradArgs {
   // instruction and z taps on the column side (form 1)
   int ARS, w8mode, w8nbv, w8nj, w8nh, w8dbg;
   int w8off[128];                     // wgrad8 row (form 0) / row-quad (form 1) A image offsets
+  // BatchNorm-backward apply of the gradient operand on load (wgrad8 form 0,
+  // when the weight gradient is the apply's only consumer): G holds d(post-
+  // BN) dz and the operand is dz*g_scale + (g_c1*g_y + g_c0) per channel, the
+  // bits bn_bwd_apply would have stored; null: G is the operand itself.
+  const float *g_y, *g_scale, *g_c1, *g_c0;
 };
 int plan_bwgrad(WGradArgs &a, int target_blocks);
 int launch_bwgrad(const WGradArgs &a, hipStream_t s);
+bool bwgrad_gap_ok(const WGradArgs &a);   // a GAP (operand-apply) instance exists
 int plan_wgrad(WGradArgs &a, int target_blocks);
 int plan_wgrad8(WGradArgs &a);
 int launch_wgrad8(const WGradArgs &a, hipStream_t s);

@@ -500,6 +500,10 @@ struct hcu_unet_plan {
   mutable hipStream_t side = nullptr;
   mutable int side_device = -1;
   mutable hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_slot[HCU_NBUF] = {};
+  // data-parallel overlap (hcu_unet_set_grad_events): caller-owned events the
+  // backward records when the decoder's / the deep encoder levels' gradients are final
+  hipEvent_t grad_ev[2] = {nullptr, nullptr};
+  int grad_deep = -1;
   void destroy_side() const {
     if (side) (void)hipStreamDestroy(side);
     for (hipEvent_t *e : {&ev_fork, &ev_join})
@@ -925,8 +929,11 @@ bool fuse_bnbwd(const Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
 // equal within noise on MI355X, so the simpler form stays the default.
 static int bn_fin_apply(const float *part, int R, int W, const BNLayer &bn, BNCoef coef, float *G,
                         int training, int accumulate, float *dz, const float *y, int64_t nvox, int Cs,
-                        hipStream_t s, int bf) {
+                        hipStream_t s, int bf, bool apply = true) {
   static const bool sep = !(getenv("HCU_BNFA") && getenv("HCU_BNFA")[0] == '1');
+  if (!apply)   // the consumer applies dz*scale + c1*y + c0 on load (WGradArgs::g_y)
+    return launch_bn_bwd_finalize(part, R, bn.C, bn.Cs, W, bn.count, coef, G + bn.gamma, G + bn.beta,
+                                  training, accumulate, s);
   if (sep) {
     if (int e = launch_bn_bwd_finalize(part, R, bn.C, bn.Cs, W, bn.count, coef, G + bn.gamma, G + bn.beta,
                                        training, accumulate, s))
@@ -938,10 +945,27 @@ static int bn_fin_apply(const float *part, int R, int W, const BNLayer &bn, BNCo
 }
 
 int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *dz, int training,
-                 int accumulate) {
+                 int accumulate, bool apply = true) {
   const BNCoef coef = coef_at(c.sv, bnl.bn);
   return bn_fin_apply(c.part(), gconv_rows(a), a.CoutW, bnl.bn, coef, c.G, training, accumulate, dz,
-                      c.fptr(c.sv, bnl.y_off), bnl.out.vox(), bnl.out.Cs, c.s, c.bf());
+                      c.fptr(c.sv, bnl.y_off), bnl.out.vox(), bnl.out.Cs, c.s, c.bf(), apply);
+}
+
+// The layer's weight gradient can take its gradient operand as d(post-BN) dz
+// and apply the BatchNorm backward on load (wgrad8 form 0 fp32, pipelined
+// bwgrad bf16): used when
+// that weight gradient is the apply's only consumer (the first layer, no
+// input gradient), which removes a full read-modify-write pass of the
+// largest gradient tensor from the end of the backward.
+bool gap_ok(const Ctx &c, const ConvLayer &L) {
+  static const bool off = getenv("HCU_NO_GAP") && getenv("HCU_NO_GAP")[0] == '1';   // A/B
+  if (off) return false;
+  // bf16: opt-in (HCU_GAP_BF16=1).  Measured on MI355X (config 3, d0.c1): the
+  // pipelined bwgrad with the operand apply ran 253 us against 115 + 116 us for
+  // bwgrad + the separate apply (register pressure of the second operand)
+  static const bool bf_on = getenv("HCU_GAP_BF16") && getenv("HCU_GAP_BF16")[0] == '1';
+  if (c.bf()) return bf_on && bwgrad_gap_ok(L.wg);
+  return L.wg.v2 == 2 && L.wg.w8mode == 0 && L.wg.GCs <= 16;
 }
 
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
@@ -949,7 +973,8 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 // BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
-                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
+                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr,
+                  bool defer_apply = false, const ConvLayer *gap = nullptr) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
   WGradArgs w = L.wg;
@@ -957,6 +982,13 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   w.a_scale = asc;
   w.a_shift = ash;
   w.G = dy;
+  if (gap) {   // dy holds dz of gap's BatchNorm: applied on load
+    const BNCoef gc = coef_at(c.sv, gap->bn);
+    w.g_y = c.fptr(c.sv, gap->y_off);
+    w.g_scale = gc.scale;
+    w.g_c1 = gc.c1;
+    w.g_c0 = gc.c0;
+  }
   if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
   if (int e = launch_wgrad(w, c.wstream())) return e;
   WGradFinalize f{};
@@ -987,7 +1019,7 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   if (int e = launch_conv_any(a, c.s)) return e;
   if (!fused) return 0;
   tag(bnl->name, "bnbwd");
-  if (int e = finish_bnbwd(c, a, *bnl, dA, training, accumulate)) return e;
+  if (int e = finish_bnbwd(c, a, *bnl, dA, training, accumulate, !defer_apply)) return e;
   if (bn_done) *bn_done = true;
   return 0;
 }
@@ -1154,6 +1186,35 @@ int hcu_unet_plan_query(const hcu_unet_plan *p, int64_t *out_shape, int64_t *n_p
   if (n_bn) *n_bn = p->n_bn;
   if (saved_bytes) *saved_bytes = p->saved_bytes;
   if (scratch_bytes) *scratch_bytes = p->scratch_bytes;
+  return HCU_OK;
+}
+
+int hcu_unet_set_grad_events(hcu_unet_plan *p, void *ev_decoder, void *ev_deep, int deep_level) {
+  if (!p || p->is_chain) return fail(HCU_ERR_INVALID, "hcu_unet_set_grad_events: U-Net plan required");
+  if (ev_deep && (deep_level < 1 || deep_level >= p->L))
+    return fail(HCU_ERR_INVALID, "hcu_unet_set_grad_events: deep_level must be in [1, levels)");
+  p->grad_ev[0] = (hipEvent_t)ev_decoder;
+  p->grad_ev[1] = (hipEvent_t)ev_deep;
+  p->grad_deep = ev_deep ? deep_level : -1;
+  return HCU_OK;
+}
+
+int hcu_event_create(void **ev) {
+  if (!ev) return fail(HCU_ERR_INVALID, "null argument");
+  hipEvent_t e = nullptr;
+  HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  *ev = e;
+  return HCU_OK;
+}
+
+int hcu_event_destroy(void *ev) {
+  if (ev) HCU_HIP(hipEventDestroy((hipEvent_t)ev));
+  return HCU_OK;
+}
+
+int hcu_stream_wait_event(hcu_stream_t stream, void *ev) {
+  if (!ev) return fail(HCU_ERR_INVALID, "null event");
+  HCU_HIP(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev, 0));
   return HCU_OK;
 }
 
@@ -1441,6 +1502,17 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     }
     cur = sd;
   }
+  // Data-parallel overlap: every gradient of a finished group is written by
+  // the finalizes pending on the branch and by kernels the main chain issued
+  // before this point; the branch flushes, joins the chain (fork) and records.
+  auto grads_ready = [&](hipEvent_t ev) -> int {
+    if (!ev) return 0;
+    if (int e = c.flush_wgf()) return e;
+    if (int e = c.fork()) return e;
+    HCU_HIP(hipEventRecord(ev, c.wstream()));
+    return 0;
+  };
+  if (int e = grads_ready(p.grad_ev[0])) return e;   // up_steps + out_conv
   // encoder, bottleneck to first
   for (int i = p.L - 1; i >= 0; --i) {
     const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
@@ -1449,8 +1521,11 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.alloc(sb)) return e;
     float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
+    // first layer without an input gradient: its weight gradient is the only
+    // consumer of d(pre-BN y1) and applies the BatchNorm backward on load
+    const bool gap = i == 0 && !dx && gap_ok(c, c1);
     if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
-                              accumulate, &c1, training, &done1))
+                              accumulate, &c1, training, &done1, gap))
       return e;
     if (!done1)
       if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
@@ -1460,7 +1535,9 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.alloc(sa)) return e;
       dIn = c.buf(sa);
     }
-    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate)) return e;
+    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training,
+                              nullptr, false, gap && done1 ? &c1 : nullptr))
+      return e;
     if (i > 0) {
       // dIn = d(pooled): produce d(pre-BN y2_{i-1}) into a fresh slot
       int sp = 0;
@@ -1472,6 +1549,10 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = launch_from_cl(dIn, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf()))
         return e;
     }
+    // levels >= i: both convs' weight gradients and every BatchNorm of theirs
+    // (dc2[i]'s in level i+1's pooled backward, or the decoder's) are final
+    if (i == p.grad_deep && i > 0)
+      if (int e = grads_ready(p.grad_ev[1])) return e;
   }
   tag(std::string("wgrad"), "finalize");
   if (int e = c.flush_wgf()) return e;

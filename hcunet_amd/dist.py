@@ -9,7 +9,9 @@ averaged in the same collective so that every rank holds the same model (and a
 checkpoint saved by rank 0 is the job's model).  num_batches_tracked is equal
 on every rank by construction and is not reduced.
 """
+import ctypes
 import os
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -31,15 +33,97 @@ def _running_stats(module, with_stats):
            [bn.running_var for bn in bns if bn.running_var is not None]
 
 
+def _reduce(t, group, world):
+    if _avg_supported(group):
+        dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.div_(world)
+
+
+def bucket_ranges(module, deep_level, n_stats):
+    """Ranges of the flat gradient buffer (+ the statistics tail) reduced
+    separately when the reduction overlaps the backward, in the order the
+    backward finalizes them: the decoder (up_steps) + the running statistics,
+    encoder levels >= deep_level, then the rest (out_conv, the shallow
+    levels).  They partition [0, n_params + n_stats): one logical reduction.
+    None when the parameter order is not the module layout this assumes."""
+    off, up0, deep0 = 0, None, None
+    seen_up = False
+    for name, p in module.named_parameters():
+        top = name.split('.')[0]
+        if top == 'down_steps':
+            if seen_up:
+                return None
+            if deep0 is None and int(name.split('.')[1]) >= deep_level:
+                deep0 = off
+        elif top == 'up_steps':
+            if up0 is None:
+                up0 = off
+            seen_up = True
+        elif seen_up:
+            return None   # something registered after up_steps
+        off += p.numel()
+    if up0 is None or deep0 is None or not 0 < deep0 < up0:
+        return None
+    return [(up0, off + n_stats), (deep0, up0), (0, deep0)]
+
+
+def prepare_overlap(module, deep_level=None):
+    """Arm the backward of `module` (a Unet_Constructor) to record, on its
+    weight-gradient stream, when the decoder's and the deep encoder levels'
+    gradients are final (include/hcunet.h hcu_unet_set_grad_events), so
+    allreduce_gradients reduces those ranges on a communication stream while
+    the shallow levels' backward still runs.  deep_level defaults to
+    levels - 2 (the two deepest levels hold most parameters).  Returns the
+    bucket ranges, or None when the module does not have the U-Net layout."""
+    from . import _lib
+    eng = module.engine()
+    levels = len(module.down_steps)
+    if levels < 3:
+        return None
+    dl = levels - 2 if deep_level is None else int(deep_level)
+    if not 1 <= dl < levels:
+        raise ValueError('deep_level must be in [1, %d)' % levels)
+    if bucket_ranges(module, dl, 0) is None:
+        return None
+    if eng.grad_events is None:
+        evs = []
+        for _ in range(2):
+            h = ctypes.c_void_p()
+            _lib.check(_lib.lib().hcu_event_create(ctypes.byref(h)), 'prepare_overlap')
+            evs.append(h)
+        eng.grad_events = (evs[0], evs[1], dl)
+        eng._comm_stream = None
+        weakref.finalize(eng, _destroy_events, evs)
+    else:
+        eng.grad_events = (eng.grad_events[0], eng.grad_events[1], dl)
+    return bucket_ranges(module, dl, 0)
+
+
+def _destroy_events(evs):
+    try:
+        from . import _lib
+        for h in evs:
+            _lib.lib().hcu_event_destroy(h)
+    except Exception:
+        pass
+
+
 def allreduce_gradients(module, group=None, bn_stats=True):
     """Average parameter gradients (and, with bn_stats, the BatchNorm running
-    mean/var) of `module` across ranks in place, in ONE collective.
+    mean/var) of `module` across ranks in place, as ONE logical reduction.
 
     Production path: every .grad is a view of the engine's flat gradient
     buffer, which is the head of engine.comm_flat; the running statistics are
-    copied into its tail, the whole buffer is all-reduced once and the tail is
-    copied back.  Otherwise the gradients and statistics are concatenated into
-    one temporary buffer (same single collective)."""
+    copied into its tail, the whole buffer is all-reduced and the tail is
+    copied back.  After prepare_overlap (broadcast_parameters calls it) the
+    buffer is reduced in three ranges on a communication stream, each waiting
+    only for the backward's event that its gradients are final: the decoder's
+    and the deep levels' reductions run while the shallow levels' backward is
+    still executing (call this right after loss.backward(), before anything
+    synchronises).  Otherwise the gradients and statistics are concatenated
+    into one temporary buffer (one collective)."""
     if not dist.is_available() or not dist.is_initialized():
         return
     world = dist.get_world_size(group)
@@ -64,6 +148,12 @@ def allreduce_gradients(module, group=None, bn_stats=True):
         flat_ok = flat_ok and off == G.numel() and C.data_ptr() == base \
             and C.numel() >= G.numel() + nstat
     native = flat_ok and C.is_cuda and 0 < len(stats) <= 128 and all(t.is_contiguous() for t in stats)
+    ev = getattr(eng, 'grad_events', None) if eng is not None else None
+    if native and ev is not None and eng.events_recorded:
+        ranges = bucket_ranges(module, ev[2], nstat)
+        if ranges is not None and ranges[0][1] == G.numel() + nstat:
+            _allreduce_overlapped(eng, C[:G.numel() + nstat], G.numel(), stats, ranges, ev, group, world)
+            return
     if flat_ok:
         buf = C[:G.numel() + nstat]
         tail = buf[G.numel():]
@@ -73,11 +163,7 @@ def allreduce_gradients(module, group=None, bn_stats=True):
             torch.cat([t.reshape(-1) for t in stats], out=tail)
     else:
         buf = torch.cat([p.grad.reshape(-1) for p in params] + [t.reshape(-1) for t in stats])
-    if _avg_supported(group):
-        dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=group)
-    else:
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-        buf.div_(world)
+    _reduce(buf, group, world)
     off = G.numel() if flat_ok else 0
     if not flat_ok:
         for p in params:
@@ -91,6 +177,34 @@ def allreduce_gradients(module, group=None, bn_stats=True):
         k = t.numel()
         t.copy_(buf[off:off + k].view_as(t))
         off += k
+
+
+def _allreduce_overlapped(eng, buf, n_grads, stats, ranges, ev, group, world):
+    """The three ranges on the engine's communication stream: each waits for
+    the backward's event of its gradients (the last one for the whole
+    backward), the statistics move in before the first and out after the
+    last; the caller's stream then waits for the communication stream."""
+    from . import _lib
+    dev = buf.device
+    main = torch.cuda.current_stream(dev)
+    comm = getattr(eng, '_comm_stream', None)
+    if comm is None or comm.device != dev:
+        comm = eng._comm_stream = torch.cuda.Stream(dev)
+    L = _lib.lib()
+    waits = [lambda: _lib.check(L.hcu_stream_wait_event(ctypes.c_void_p(comm.cuda_stream), ev[0]),
+                                'allreduce_gradients'),
+             lambda: _lib.check(L.hcu_stream_wait_event(ctypes.c_void_p(comm.cuda_stream), ev[1]),
+                                'allreduce_gradients'),
+             lambda: comm.wait_stream(main)]
+    with torch.cuda.stream(comm):
+        for k, (lo, hi) in enumerate(ranges):
+            waits[k]()
+            if k == 0:
+                _stats_move(stats, buf[n_grads:], unpack=False)
+            _reduce(buf[lo:hi], group, world)
+        _stats_move(stats, buf[n_grads:], unpack=True)
+    main.wait_stream(comm)
+    eng.events_recorded = False
 
 
 def _stats_move(stats, buf, unpack):
@@ -124,3 +238,6 @@ def broadcast_parameters(module, src=0, group=None):
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src=src, group=group)
+    if os.environ.get('HCU_DP_OVERLAP', '1') != '0' and hasattr(module, 'engine') \
+            and next(module.parameters()).is_cuda:
+        prepare_overlap(module)

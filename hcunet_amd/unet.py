@@ -401,6 +401,11 @@ class _Engine:
         self._slots = None   # (module, name) of each parameter, in self.params order
         self._bns = None
         self._bn_arrays = None
+        # data-parallel overlap (hcunet_amd.dist.prepare_overlap): native events
+        # the backward records when gradient groups are final, and whether the
+        # last backward recorded them into grad_flat
+        self.grad_events = None      # (ev_decoder, ev_deep, deep_level) or None
+        self.events_recorded = False
 
     def check_input(self, x, bf16=False):
         m = self.module_ref
@@ -621,6 +626,11 @@ class _UnetFunction(torch.autograd.Function):
         dx = torch.empty(x.shape, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
         G, accumulate, finish = eng.grad_target()
         t = eng.tensors(x, None, saved, scratch, grads=G)
+        ev = eng.grad_events if G is eng.grad_flat else None
+        _lib.check(_lib.lib().hcu_unet_set_grad_events(
+            plan.handle, ev[0] if ev else None, ev[1] if ev else None, ev[2] if ev else 0),
+            'Unet_Constructor.backward')
+        eng.events_recorded = ev is not None
         with torch.cuda.device(dev):
             _lib.check(_lib.lib().hcu_unet_backward(plan.handle, ctypes.byref(t),
                                                     ctypes.c_void_p(dout.data_ptr()),

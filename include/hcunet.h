@@ -224,6 +224,19 @@ int hcu_gate_fwd(const float *hp, const float *zp, const float *h_prev, float *o
 int hcu_gate_bwd(const float *hp, const float *zp, const float *h_prev, const float *dout, float *dhp,
                  float *dzp, float *dh_prev, int64_t n, hcu_stream_t stream);
 
+/* Data-parallel overlap (hcunet_amd/dist.py): with events set, every later  */
+/* hcu_unet_backward on `plan` records ev_decoder on its weight-gradient     */
+/* stream once the decoder's parameter gradients (up_steps, out_conv) are    */
+/* final, and ev_deep once those of encoder levels >= deep_level are, so a   */
+/* caller can reduce those gradient ranges while the rest of the backward    */
+/* runs (hcu_stream_wait_event on its communication stream).  Each event    */
+/* costs one extra batched weight-gradient finalize launch.  NULL events:    */
+/* nothing recorded (the default).  The events stay owned by the caller.     */
+int hcu_unet_set_grad_events(hcu_unet_plan *plan, void *ev_decoder, void *ev_deep, int deep_level);
+int hcu_event_create(void **ev);          /* hipEventDisableTiming */
+int hcu_event_destroy(void *ev);
+int hcu_stream_wait_event(hcu_stream_t stream, void *ev);
+
 /* Data parallel (hcunet_amd/dist.py): n <= 128 fp32 vectors (the BatchNorm
  * running statistics) gathered into (unpack = 0) or scattered from
  * (unpack = 1) one contiguous buffer in one launch, in order. */

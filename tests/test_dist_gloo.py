@@ -138,3 +138,66 @@ def test_dp_allreduce_matches_mean_of_shard_grads():
         assert not torch.equal(lrs0[k], lrs1[k]) or 'var' in k, k   # shards differ
         assert torch.equal(rs0[k], rs1[k]), k
         assert torch.allclose(rs0[k], (lrs0[k] + lrs1[k]) / 2, rtol=1e-6, atol=1e-9), k
+
+
+def test_bucket_ranges_partition_the_communication_buffer():
+    """dist.bucket_ranges: decoder + statistics tail, deep encoder levels, rest
+    (out_conv and the shallow levels) -- contiguous, disjoint, covering
+    [0, n_params + n_stats), each range holding exactly its modules' params."""
+    from hcat.unet import Unet_Constructor
+    from hcunet_amd import dist as hd
+    kw = dict(KW, feature_sizes=[8, 16, 32, 64, 128])
+    m = Unet_Constructor(**kw)
+    n = sum(p.numel() for p in m.parameters())
+    r = hd.bucket_ranges(m, 3, 100)
+    (d0, d1), (e0, e1), (s0, s1) = r
+    assert (s0, s1, e1, d1) == (0, e0, d0, n + 100)
+    off = 0
+    for name, p in m.named_parameters():
+        lo, hi = off, off + p.numel()
+        off = hi
+        if name.startswith('up_steps'):
+            assert d0 <= lo and hi <= d1, name
+        elif name.startswith('down_steps') and int(name.split('.')[1]) >= 3:
+            assert e0 <= lo and hi <= e1, name
+        else:
+            assert s0 <= lo and hi <= s1, name
+    assert hd.bucket_ranges(Unet_Constructor(**KW), 3, 0) is None   # 2 levels: no deep range
+
+
+def _ranges_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hcunet_amd import dist as hd
+        g = torch.Generator().manual_seed(rank)
+        buf = torch.randn(1000, generator=g)
+        whole = buf.clone()
+        hd._reduce(whole, None, world)
+        for lo, hi in [(600, 1000), (250, 600), (0, 250)]:
+            hd._reduce(buf[lo:hi], None, world)
+        q.put((rank, whole.numpy().copy(), buf.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reduction_in_ranges_equals_one_reduction():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ranges_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, whole, parts = q.get(timeout=120)
+        res[r] = (whole, parts)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import numpy as np
+    for r in (0, 1):
+        np.testing.assert_array_equal(res[r][0], res[r][1])
+    np.testing.assert_array_equal(res[0][1], res[1][1])

@@ -1,10 +1,14 @@
 """Data-parallel step on the GPU path, world size 2 over gloo with both ranks
 on cuda:0 (the 8-GPU RCCL run is the driver's): real native forward/backward
-per batch shard, then hcunet_amd.dist.allreduce_gradients -- ONE collective
-over the flat gradient buffer + BatchNorm running statistics, the statistics
-moved in and out of it by one kernel each (hcu_gather_vectors).  Checks: one
-collective, rank-symmetric results, reduced = mean of the per-rank values, and
-the deterministic tiling mode every rank plans with."""
+per batch shard, then hcunet_amd.dist.allreduce_gradients -- ONE logical
+reduction of the flat gradient buffer + BatchNorm running statistics, the
+statistics moved in and out of it by one kernel each (hcu_gather_vectors):
+either one collective (HCU_DP_OVERLAP=0) or, by default, three ranges on a
+communication stream that wait for the backward's gradient-ready events
+(decoder, deep levels, rest) -- a partition of the same buffer.  Checks: the
+collectives cover the buffer exactly once, rank-symmetric results, reduced =
+mean of the per-rank values, both modes agree bitwise, and the deterministic
+tiling mode every rank plans with."""
 import os
 import socket
 
@@ -31,9 +35,10 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap):
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
+    os.environ['HCU_DP_OVERLAP'] = '1' if overlap else '0'
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         from hcat.loss import cross_entropy
@@ -75,11 +80,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_dp_step_on_gpu_one_collective_rank_symmetric():
+def _run(overlap):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     res = {}
@@ -89,11 +94,31 @@ def test_dp_step_on_gpu_one_collective_rank_symmetric():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+def test_dp_step_on_gpu_one_collective_rank_symmetric():
+    import numpy as np
+    res = _run(False)
+    _check(res, overlapped=False)
+    res_ov = _run(True)
+    _check(res_ov, overlapped=True)
+    for r in (0, 1):   # the overlapped ranges reduce the same values: bitwise equal
+        for a, b in zip(res[r][1:4], res_ov[r][1:4]):
+            for k in a:
+                np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def _check(res, overlapped):
     (loc0, red0, lrs0, rs0, calls0, mode0, nbn), (loc1, red1, lrs1, rs1, calls1, mode1, _) = res[0], res[1]
     import numpy as np
     n_params = sum(v.size for v in loc0.values())
     n_stats = sum(v.size for v in rs0.values())
-    assert calls0 == [n_params + n_stats] == calls1
+    assert calls0 == calls1
+    if overlapped:   # decoder + statistics, deep levels, rest: a partition
+        assert len(calls0) == 3 and sum(calls0) == n_params + n_stats, calls0
+    else:
+        assert calls0 == [n_params + n_stats]
     assert mode0 == mode1 == 1          # the deterministic tiling mode
     for n in red0:
         np.testing.assert_array_equal(red0[n], red1[n])
