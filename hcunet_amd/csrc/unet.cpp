@@ -21,6 +21,7 @@
 #include "timing.h"
 #include "../../include/hcunet.h"
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -772,6 +773,16 @@ int build_plan(hcu_unet_plan &p) {
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
   p.fin_off = scratch.take_floats(16);
   p.scratch_bytes = scratch.off;
+  if (getenv("HCU_PLAN_LOG")) {   // weight-gradient kernels and their partial slabs (measurement)
+    auto wlog = [](const std::string &n, const WGradArgs &w) {
+      const char *k = w.use_bw ? "bwgrad" : w.v2 == 2 ? "wgrad8" : w.v2 == 1 ? "wgrad2" : "wgrad";
+      fprintf(stderr, "wgrad %-8s %-7s KB %5d M %5d N %4d slabs %7.2f MB grid %d x %d x %d\n", n.c_str(), k,
+              w.KB, w.Mtot, w.Ntot, 4e-6 * w.KB * (double)w.Mtot * w.Ntot, w.KB, w.mchunks, w.nchunks);
+    };
+    for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
+      for (const ConvLayer &cl : *v) wlog(cl.name, cl.wg);
+    for (const ConvTLayer &u : p.up) wlog(u.name, u.wg);
+  }
   return 0;
 }
 
