@@ -10,8 +10,8 @@ for C in $CFGS; do
     i=0
     for E in "X_BASE=1" "$@"; do
       env $E timeout -k 10 200 python -u bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing \
-        > $O/${TAG}_$C_$i.json 2> $O/${TAG}_$C_$i.err || { tail -20 $O/${TAG}_$C_$i.err; exit 1; }
-      python3 -c "import json;d=json.loads(open('$O/${TAG}_$C_$i.json').read().strip().splitlines()[-1]);print('config $C run $r [$E] ms/step',round(d['ms_per_step'],4),'host',round(d['config']['host_enqueue_ms_per_step'],3))"
+        > $O/${TAG}_${C}_${i}.json 2> $O/${TAG}_${C}_${i}.err || { tail -20 $O/${TAG}_${C}_${i}.err; exit 1; }
+      python3 -c "import json;d=json.loads(open('$O/${TAG}_${C}_${i}.json').read().strip().splitlines()[-1]);print('config $C run $r [$E] ms/step',round(d['ms_per_step'],4),'host',round(d['config']['host_enqueue_ms_per_step'],3))"
       i=$((i+1))
     done
   done
