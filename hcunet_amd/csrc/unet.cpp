@@ -432,7 +432,8 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 
 }  // namespace
 
-#define HCU_NBUF 6
+#define HCU_NBUF 32   // gradient slots (at most; Ctx::alloc)
+#define HCU_NBUF_RING 6   // ring size when one slot per allocation does not fit
 
 struct hcu_unet_plan {
   hcu_unet_spec spec;
@@ -460,6 +461,11 @@ struct hcu_unet_plan {
   // a slot read by the weight-gradient branch is rewritten only several
   // layers later (see Ctx::alloc).
   size_t buf_off[HCU_NBUF] = {};
+  // slots in use: one per allocation of a U-Net backward when they fit (no
+  // slot is rewritten, so no reader events or waits on the gradient ring),
+  // else a ring of HCU_NBUF_RING (chains, very large activations)
+  int nbuf = HCU_NBUF_RING;
+  bool no_reuse = false;
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
   size_t fin_off = 0;   // fused BatchNorm finalize ticket counter (zeroed per forward)
   double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
@@ -763,7 +769,16 @@ int build_plan(hcu_unet_plan &p) {
   Region scratch;
   // the gradient ring, the weight-gradient partials and the weight re-layout
   // scratch are backward-only
-  for (size_t &b : p.buf_off) b = scratch.take_floats(fwd_only ? 0 : p.max_act);
+  {
+    // a U-Net backward allocates 1 + 3 slots per decoder level + at most 3 per
+    // encoder level: one slot each when that stays within 32 slots and 24 GB
+    const int need = 1 + 3 * (L - 1) + 3 * L;
+    p.no_reuse = !fwd_only && need <= HCU_NBUF && (double)need * p.max_act * 4.0 <= 24e9 &&
+                 !(getenv("HCU_GRAD_RING") && getenv("HCU_GRAD_RING")[0] == '1');   // A/B
+    p.nbuf = p.no_reuse ? need : HCU_NBUF_RING;
+    for (int i = 0; i < HCU_NBUF; ++i)
+      p.buf_off[i] = scratch.take_floats(fwd_only || i >= p.nbuf ? 0 : p.max_act);
+  }
   p.part_off = scratch.take_floats(p.max_part);
   // the slab arena holds several layers' weight-gradient partials until their
   // finalizes run together (at least one layer's, at most 8 M floats beyond)
@@ -843,7 +858,7 @@ struct Ctx {
   // Fresh slot for the main chain to write; waits for the branch's last read of it.
   int alloc(int &slot) {
     slot = next_slot;
-    next_slot = (next_slot + 1) % HCU_NBUF;
+    next_slot = (next_slot + 1) % p.nbuf;
     if (split && (slot_read & (1u << slot))) HCU_HIP(hipStreamWaitEvent(s, p.ev_slot[slot], 0));
     return HCU_OK;
   }
@@ -856,7 +871,7 @@ struct Ctx {
   }
   // The branch work issued so far is the last reader of `slot`.
   int read_done(int slot) {
-    if (!split || slot < 0) return HCU_OK;
+    if (!split || slot < 0 || p.no_reuse) return HCU_OK;   // no_reuse: never rewritten
     HCU_HIP(hipEventRecord(p.ev_slot[slot], ws));
     slot_read |= 1u << slot;
     return HCU_OK;
@@ -2082,7 +2097,7 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
     (j.kind == PREP_CONV_DGRAD || j.kind == PREP_CONVT_DGRAD ? p.prep_bwd : p.prep_fwd).push_back(j);
   p.saved_bytes = saved.off;
   Region scratch;
-  for (size_t &b : p.buf_off) b = scratch.take_floats(p.max_act);
+  for (int i = 0; i < HCU_NBUF; ++i) p.buf_off[i] = scratch.take_floats(i < p.nbuf ? p.max_act : 0);
   p.part_off = scratch.take_floats(p.max_part);
   p.wpart_floats = std::max<size_t>(p.max_part, (size_t)1 << 20);
   p.wpart_off = scratch.take_floats(p.wpart_floats);
