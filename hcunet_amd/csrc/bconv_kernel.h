@@ -148,6 +148,9 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   constexpr int TPS = 4 / CV;          // taps per K-step
   constexpr int CKP = ckp_bytes(CV) / ES;   // halo row stride (elements)
   E *const tag = nullptr;              // overload selector
+#ifdef HCU_BCONV_PHASES
+  const long long ph_start = (long long)__builtin_readcyclecounter();
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   if (tid == 0) sa = a;
@@ -531,6 +534,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #ifdef HCU_BCONV_PHASES
   long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
   long long ph_t = (long long)__builtin_readcyclecounter();
+  if (tid == 0) atomicAdd(&g_bconv_phase[6], (unsigned long long)(ph_t - ph_start));   // prologue
 #endif
   if (NPF > 0) {
     int tile = t_beg;
@@ -614,7 +618,13 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // lanes of each channel group, then the 4 waves' (S1, S2, K, n) merged in a
   // fixed order by the parallel-variance identity about the first non-empty
   // wave's pivot (fused BatchNorm backward: plain sums)
-  if (!a.stats || split) return;
+  if (!a.stats || split) {
+#ifdef HCU_BCONV_PHASES
+    if (tid == 0)
+      atomicAdd(&g_bconv_phase[7], (unsigned long long)((long long)__builtin_readcyclecounter() - ph_start));
+#endif
+    return;
+  }
 #pragma unroll
   for (int m = 1; m < 16; m <<= 1) {
     cnt += __shfl_xor(cnt, m);
@@ -675,6 +685,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       if (tid == 0) bn_fin_reset(a.fin.counter);
     }
   }
+#ifdef HCU_BCONV_PHASES
+  if (tid == 0)   // whole block lifetime of wave 0 (prologue + loop + statistics)
+    atomicAdd(&g_bconv_phase[7], (unsigned long long)((long long)__builtin_readcyclecounter() - ph_start));
+#endif
 #undef KA
 }
 

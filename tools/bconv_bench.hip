@@ -171,5 +171,8 @@ int main(int argc, char **argv) {
            "epilogue %.0f  total %.0f (tiles/launch %.0f)\n",
            ph[0] / tiles, ph[1] / tiles, ph[2] / tiles, ph[3] / tiles, ph[4] / tiles, tot / tiles,
            tiles / iters);
+  const double blocks = (double)a.gridx * (a.CoutW / (a.NSUB * 16)) * a.ksplit * iters;
+  printf("  per block (wave 0, cycles): prologue %.0f  lifetime %.0f (blocks/launch %.0f)\n", ph[6] / blocks,
+         ph[7] / blocks, blocks / iters);
   return 0;
 }
