@@ -15,7 +15,7 @@
 namespace hcu {
 
 #ifdef HCU_BCONV_PHASES
-__device__ unsigned long long g_bconv_phase[8];
+__device__ unsigned long long g_bconv_phase[kPhBlocks * kPhN];
 #endif
 
 // ---------------------------------------------------------------------------

@@ -50,7 +50,10 @@ namespace hcu {
 // Per-phase cycle totals of wave 0 of every block (tools/bconv_bench only):
 // [0] halo -> LDS (incl. the wait for the prefetch), [1] barrier + weights,
 // [2] next-halo issue, [3] MFMA loop, [4] epilogue, [5] tiles.
-extern __device__ unsigned long long g_bconv_phase[8];
+// per block slot (plain stores, no atomics: blocks of successive launches with
+// the same index run one after another) of kPhN counters
+constexpr int kPhBlocks = 8192, kPhN = 12;
+extern __device__ unsigned long long g_bconv_phase[kPhBlocks * kPhN];
 #define PH_MARK(k)                                                 \
   do {                                                             \
     const long long t__ = (long long)__builtin_readcyclecounter(); \
@@ -534,7 +537,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #ifdef HCU_BCONV_PHASES
   long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
   long long ph_t = (long long)__builtin_readcyclecounter();
-  if (tid == 0) atomicAdd(&g_bconv_phase[6], (unsigned long long)(ph_t - ph_start));   // prologue
+  const long long ph_loop0 = ph_t;   // prologue = ph_loop0 - ph_start
 #endif
   if (NPF > 0) {
     int tile = t_beg;
@@ -610,8 +613,21 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
   }
 #ifdef HCU_BCONV_PHASES
-  if (tid == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_bconv_phase[k], (unsigned long long)ph_acc[k]);
+  const long long ph_loop1 = (long long)__builtin_readcyclecounter();
+  long long ph_post[3] = {ph_loop1, ph_loop1, ph_loop1};
+  auto ph_flush = [&]() {
+    if (tid != 0) return;
+    const long long t_end = (long long)__builtin_readcyclecounter();
+    const int slot = ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) % kPhBlocks;
+    unsigned long long *d = g_bconv_phase + (size_t)slot * kPhN;
+    for (int k = 0; k < 6; ++k) d[k] += (unsigned long long)ph_acc[k];
+    d[6] += (unsigned long long)(ph_loop0 - ph_start);   // prologue
+    d[7] += (unsigned long long)(t_end - ph_start);      // lifetime
+    d[8] += (unsigned long long)(ph_post[0] - ph_loop1); // post-loop: shuffles
+    d[9] += (unsigned long long)(ph_post[1] - ph_post[0]);  // LDS merge (2 barriers)
+    d[10] += (unsigned long long)(ph_post[2] - ph_post[1]); // row merge + store
+    d[11] += (unsigned long long)(t_end - ph_post[2]);
+  };
 #endif
 
   // ---- statistics row of the block: fixed-order butterfly over the 16 voxel
@@ -620,8 +636,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // wave's pivot (fused BatchNorm backward: plain sums)
   if (!a.stats || split) {
 #ifdef HCU_BCONV_PHASES
-    if (tid == 0)
-      atomicAdd(&g_bconv_phase[7], (unsigned long long)((long long)__builtin_readcyclecounter() - ph_start));
+    ph_flush();
 #endif
     return;
   }
@@ -636,6 +651,9 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
         st2[n][r] += __shfl_xor(st2[n][r], m);
       }
   }
+#ifdef HCU_BCONV_PHASES
+  ph_post[0] = ph_post[1] = ph_post[2] = (long long)__builtin_readcyclecounter();
+#endif
   lds_barrier();   // the halo region is free: [4 waves][NT] of (S1, S2, n)
   float *mrg = smem;
   if (r16 == 0)
@@ -649,6 +667,9 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
         e[2] = cnt;
       }
   lds_barrier();
+#ifdef HCU_BCONV_PHASES
+  ph_post[1] = ph_post[2] = (long long)__builtin_readcyclecounter();
+#endif
   for (int col = tid; col < NT; col += 256) {
     if (co0 + col >= a.OCs) continue;
     float S1 = 0.f, S2 = 0.f, nn = 0.f, K = 0.f;
@@ -679,6 +700,9 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     else
       *reinterpret_cast<float2 *>(a.stats + c * 2) = make_float2(S1, S2);
   }
+#ifdef HCU_BCONV_PHASES
+  ph_post[2] = (long long)__builtin_readcyclecounter();
+#endif
   if (fwdstat && a.fin.counter) {   // fused BatchNorm finalize (BnFin, common.h)
     if (bn_fin_ticket(a.fin.counter, reinterpret_cast<int *>(smem))) {
       bn_fwd_finalize_tail(a.stats, a.fin, reinterpret_cast<double *>(smem));
@@ -686,8 +710,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
   }
 #ifdef HCU_BCONV_PHASES
-  if (tid == 0)   // whole block lifetime of wave 0 (prologue + loop + statistics)
-    atomicAdd(&g_bconv_phase[7], (unsigned long long)((long long)__builtin_readcyclecounter() - ph_start));
+  ph_flush();
 #endif
 #undef KA
 }

@@ -141,8 +141,8 @@ int main(int argc, char **argv) {
   for (int i = 0; i < 3; ++i)
     if (launch_bconv(a, s)) return 1;
   CK_HIP(hipStreamSynchronize(s));
-  unsigned long long z[8] = {0};
-  CK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bconv_phase), z, sizeof(z)));
+  std::vector<unsigned long long> z(kPhBlocks * kPhN, 0ull);
+  CK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_bconv_phase), z.data(), z.size() * 8));
   hipEvent_t e0, e1;
   CK_HIP(hipEventCreate(&e0));
   CK_HIP(hipEventCreate(&e1));
@@ -152,8 +152,10 @@ int main(int argc, char **argv) {
   CK_HIP(hipEventSynchronize(e1));
   float ms = 0.f;
   CK_HIP(hipEventElapsedTime(&ms, e0, e1));
-  unsigned long long ph[8];
-  CK_HIP(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_bconv_phase), sizeof(ph)));
+  CK_HIP(hipMemcpyFromSymbol(z.data(), HIP_SYMBOL(g_bconv_phase), z.size() * 8));
+  unsigned long long ph[kPhN] = {0};
+  for (int b = 0; b < kPhBlocks; ++b)
+    for (int k = 0; k < kPhN; ++k) ph[k] += z[(size_t)b * kPhN + k];
   const double us = ms * 1e3 / iters;
   const double flops = 2.0 * B * a.OX * a.OY * a.OZ * (double)Cout * T * ICs;
   const double bytes = (double)ES * (n_in + n_out) + (bnbwd ? (double)ES * n_out : 0.0);
@@ -172,7 +174,8 @@ int main(int argc, char **argv) {
            ph[0] / tiles, ph[1] / tiles, ph[2] / tiles, ph[3] / tiles, ph[4] / tiles, tot / tiles,
            tiles / iters);
   const double blocks = (double)a.gridx * (a.CoutW / (a.NSUB * 16)) * a.ksplit * iters;
-  printf("  per block (wave 0, cycles): prologue %.0f  lifetime %.0f (blocks/launch %.0f)\n", ph[6] / blocks,
-         ph[7] / blocks, blocks / iters);
+  printf("  per block (wave 0, cycles): prologue %.0f  lifetime %.0f  post-loop: shuffles %.0f  lds merge %.0f"
+         "  rows %.0f  tail %.0f (blocks/launch %.0f)\n", ph[6] / blocks, ph[7] / blocks, ph[8] / blocks,
+         ph[9] / blocks, ph[10] / blocks, ph[11] / blocks, blocks / iters);
   return 0;
 }
