@@ -226,13 +226,9 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
     // A rows are 0 (staged as outside), so nothing else is needed.
     lds_barrier();
     for (int p0 = 0; p0 < PT; p0 += 32) {
-      // voxel order inside the K-step: k = 8g + j <-> voxel 4g + j (j < 4, the lo
-      // read) / 16 + 4g + j - 4 (hi): one LDS cycle (lanes 0-31) of a
-      // transposed read then touches 8 consecutive halo rows, which the
-      // plan's row strides (bwgrad_row_stride) spread over all 64 banks
-      const int pr = p0 + 4 * g + q4;
-      const int ra0 = hvA[pr], ra1 = hvA[pr + 16];
-      const int rg0 = hvG[pr], rg1 = hvG[pr + 16];
+      const int pr = p0 + 8 * g + q4;
+      const int ra0 = hvA[pr], ra1 = hvA[pr + 4];
+      const int rg0 = hvG[pr], rg1 = hvG[pr + 4];
       shortx8 bf[NS];
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
@@ -519,13 +515,9 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     if (tt + 1 < t_end) load(tt + 1);   // in flight during this tile's MFMAs
     lds_barrier();
     for (int p0 = 0; p0 < PT; p0 += 32) {
-      // voxel order inside the K-step: k = 8g + j <-> voxel 4g + j (j < 4, the lo
-      // read) / 16 + 4g + j - 4 (hi): one LDS cycle (lanes 0-31) of a
-      // transposed read then touches 8 consecutive halo rows, which the
-      // plan's row strides (bwgrad_row_stride) spread over all 64 banks
-      const int pr = p0 + 4 * g + q4;
-      const int ra0 = hvA[pr], ra1 = hvA[pr + 16];
-      const int rg0 = hvG[pr], rg1 = hvG[pr + 16];
+      const int pr = p0 + 8 * g + q4;
+      const int ra0 = hvA[pr], ra1 = hvA[pr + 4];
+      const int rg0 = hvG[pr], rg1 = hvG[pr + 4];
       shortx8 bf[NS];
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
@@ -593,16 +585,6 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Row stride (bf16 elements) of an LDS image with C channels per row such that
-// 8 consecutive rows of one ds_read_b64_tr_b16 LDS cycle (lanes 0-31: 8 rows x
-// 8 dwords) hit 64 distinct banks: the stride in dwords must be an odd
-// multiple of 8 (MI355X_MICROARCH.md LDS table: bank = dword address mod 64).
-static int bwgrad_row_stride(int C) {
-  int m = (C + 15) / 16;
-  if (m % 2 == 0) ++m;
-  return 16 * m;
-}
-
 int plan_bwgrad(WGradArgs &a, int target_blocks) {
   a.use_bw = 0;
   const int T = a.KX * a.KY * a.KZ;
@@ -655,19 +637,11 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   // voxel tile: TX*TY = 32 (or 64 when the halo fits), TZ = the whole Z (<= 16)
   const int ntz = cdiv(a.PZ, 16);
   a.TZ = cdiv(a.PZ, ntz);
+  a.PA2 = a.CKA + 8;
+  a.PG2 = a.CKG + 8;
   const int txys[3][2] = {{8, 8}, {4, 8}, {4, 8}};
   long lds = 0;
   const int t0i = getenv("HCU_BW_TILE") ? std::max(0, std::min(2, atoi(getenv("HCU_BW_TILE")))) : 0;
-  // Row strides (bf16 elements) of the A halo / G images: conflict-free ones
-  // first (bwgrad_row_stride), the compact C + 8 where those do not fit
-  static const bool compact_only = getenv("HCU_BW_COMPACT") && getenv("HCU_BW_COMPACT")[0] == '1';   // A/B
-  const int strides[4][2] = {{bwgrad_row_stride(a.CKA), bwgrad_row_stride(a.CKG)},
-                             {bwgrad_row_stride(a.CKA), a.CKG + 8},
-                             {a.CKA + 8, bwgrad_row_stride(a.CKG)},
-                             {a.CKA + 8, a.CKG + 8}};
-  for (int si = compact_only ? 3 : 0; si < 4; ++si) {
-  a.PA2 = strides[si][0];
-  a.PG2 = strides[si][1];
   for (int i = t0i; i < 3; ++i) {
     a.TX = txys[i][0];
     a.TY = txys[i][1];
@@ -682,8 +656,6 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
     a.PTV = a.TX * a.TY * a.TZ;
     lds = ((long)a.HAV * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
     if (lds <= 80 * 1024) break;
-  }
-  if (lds <= 160 * 1024) break;
   }
   if (lds > 160 * 1024) return fail(4, "bwgrad: tile does not fit LDS");
   a.lds_bytes = (int)((lds + 15) & ~15L);
