@@ -850,11 +850,11 @@ int launch_bconv_f32(const GConvArgs &a, hipStream_t s);
   if (cv == CV_ && a.NSUB == NS_ && a.MPW == MP_ && a.NPF == PF_) {                                  \
     if (a.bn_y)                                                                                      \
       HCU_TIMED(s, "bconv_kernel<" TAG_ "," #CV_ "," #NS_ "," #MP_ "," #PF_ ",bnb>", fl, by,         \
-                hipLaunchKernelGGL((bconv_kernel<E_, CV_, NS_, MP_, PF_, true>), grid, dim3(256),    \
+                HCU_LAUNCH((bconv_kernel<E_, CV_, NS_, MP_, PF_, true>), grid, dim3(256),    \
                                    a.lds_bytes - (int)sizeof(GConvArgs), s, a));                     \
     else                                                                                             \
       HCU_TIMED(s, "bconv_kernel<" TAG_ "," #CV_ "," #NS_ "," #MP_ "," #PF_ ">", fl, by,             \
-                hipLaunchKernelGGL((bconv_kernel<E_, CV_, NS_, MP_, PF_, false>), grid, dim3(256),   \
+                HCU_LAUNCH((bconv_kernel<E_, CV_, NS_, MP_, PF_, false>), grid, dim3(256),   \
                                    a.lds_bytes - (int)sizeof(GConvArgs), s, a));                     \
     launched = true;                                                                                 \
   }
@@ -887,7 +887,7 @@ int launch_bconv_f32(const GConvArgs &a, hipStream_t s);
     const int vpb = bconv_reduce_vpb(a);                                                             \
     const int blocks = (int)((nvox + vpb - 1) / vpb);                                                \
     HCU_TIMED(s, "bconv_reduce_kernel<" TAG_ ">", 0.0, (4.0 * a.ksplit + 2.0) * a.slice_floats,      \
-              hipLaunchKernelGGL(bconv_reduce_kernel<E_>, dim3(blocks), dim3(256), 0, s, a, vpb));   \
+              HCU_LAUNCH(bconv_reduce_kernel<E_>, dim3(blocks), dim3(256), 0, s, a, vpb));   \
     HCU_CHECK_LAUNCH();                                                                              \
   }                                                                                                  \
   return 0;

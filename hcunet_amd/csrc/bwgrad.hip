@@ -716,14 +716,14 @@ int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
 #define BWP(MS_, NS_, NP_)                                                                  \
   if (!ok && a.NPA == NP_ && !a.g_y) {                                                      \
     HCU_TIMED(s, "bwgrad_pipe_kernel<" #MS_ "," #NS_ "," #NP_ ">", fl, by,                    \
-              hipLaunchKernelGGL((bwgrad_pipe_kernel<MS_, NS_, NP_, false>), grid, dim3(256),  \
+              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_, false>), grid, dim3(256),  \
                                  a.lds_bytes, s, a));                                       \
     ok = true;                                                                              \
   }
 #define BWPG(MS_, NS_, NP_)                                                                 \
   if (!ok && a.NPA == NP_ && a.g_y && a.MSW == MS_ && a.NSB <= NS_) {                       \
     HCU_TIMED(s, "bwgrad_pipe_kernel<" #MS_ "," #NS_ "," #NP_ ",gap>", fl, by,                \
-              hipLaunchKernelGGL((bwgrad_pipe_kernel<MS_, NS_, NP_, true>), grid, dim3(256),   \
+              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_, true>), grid, dim3(256),   \
                                  a.lds_bytes, s, a));                                       \
     ok = true;                                                                              \
   }
@@ -736,7 +736,7 @@ int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
     BWP(MS_, NS_, 8) BWP(MS_, NS_, 16) BWP(MS_, NS_, 32)                                    \
     if (!ok) {                                                                              \
       HCU_TIMED(s, "bwgrad_kernel<" #MS_ "," #NS_ ">", fl, by,                              \
-                hipLaunchKernelGGL((bwgrad_kernel<MS_, NS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+                HCU_LAUNCH((bwgrad_kernel<MS_, NS_>), grid, dim3(256), a.lds_bytes, s, a)); \
     }                                                                                       \
     ok = true;                                                                              \
   }

@@ -828,7 +828,7 @@ int conv2_stat_rows(const GConvArgs &a) {
 #define CONV2_CASE(CK_, NS_, MP_, PF_)                                                         \
   if (a.CK == CK_ && a.NSUB == NS_ && a.MPW == MP_ && a.NPF == PF_) {                           \
     HCU_TIMED(s, "conv2_kernel<" #CK_ "," #NS_ "," #MP_ "," #PF_ ">", fl, by,                     \
-              hipLaunchKernelGGL((conv2_kernel<CK_, NS_, MP_, PF_>), grid, dim3(256),           \
+              HCU_LAUNCH((conv2_kernel<CK_, NS_, MP_, PF_>), grid, dim3(256),           \
                                  a.lds_bytes, s, a));                                           \
     launched = true;                                                                            \
   }
@@ -855,7 +855,7 @@ int launch_conv2(const GConvArgs &a, hipStream_t s) {
     const int vpb = reduce_vox_per_block(a);
     const int blocks = (int)((nvox + vpb - 1) / vpb);
     HCU_TIMED(s, "conv2_reduce_kernel", 0.0, 4.0 * (double)(a.ksplit + 1) * a.slice_floats,
-              hipLaunchKernelGGL(conv2_reduce_kernel, dim3(blocks), dim3(256), 0, s, a, vpb));
+              HCU_LAUNCH(conv2_reduce_kernel, dim3(blocks), dim3(256), 0, s, a, vpb));
     HCU_CHECK_LAUNCH();
   }
   return 0;

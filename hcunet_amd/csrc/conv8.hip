@@ -433,11 +433,11 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   if (C4 == C4_ && a.G8 == G_ && a.NPF == NPF_) {                                                \
     if (a.bn_y)                                                                                  \
       HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ",bnb>", fl, by,                       \
-                hipLaunchKernelGGL((conv8_kernel<C4_, G_, NPF_, true>), dim3(a.gridx), dim3(256), \
+                HCU_LAUNCH((conv8_kernel<C4_, G_, NPF_, true>), dim3(a.gridx), dim3(256), \
                                    a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
     else                                                                                         \
       HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ">", fl, by,                           \
-                hipLaunchKernelGGL((conv8_kernel<C4_, G_, NPF_, false>), dim3(a.gridx), dim3(256), \
+                HCU_LAUNCH((conv8_kernel<C4_, G_, NPF_, false>), dim3(a.gridx), dim3(256), \
                                    a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
     launched = true;                                                                             \
   }

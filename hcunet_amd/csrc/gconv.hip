@@ -313,7 +313,7 @@ int plan_gconv(GConvArgs &a, int target_blocks) {
 #define GCONV_CASE(CK_, NS_, MP_)                                                            \
   if (a.CK == CK_ && a.NSUB == NS_ && a.MPW == MP_) {                                        \
     HCU_TIMED(s, "gconv_kernel<" #CK_ "," #NS_ "," #MP_ ">", gconv_flops(a), gconv_bytes(a),  \
-              hipLaunchKernelGGL((gconv_kernel<CK_, NS_, MP_>), grid, dim3(256), a.lds_bytes, \
+              HCU_LAUNCH((gconv_kernel<CK_, NS_, MP_>), grid, dim3(256), a.lds_bytes, \
                                  s, a));                                                     \
     HCU_CHECK_LAUNCH();                                                                      \
     return 0;                                                                                \

@@ -111,17 +111,17 @@ extern "C" int hcu_ingest_volume(const void *src, int src_dtype, int B, int Z, i
   switch (src_dtype) {
     case HCU_U16:
       HCU_TIMED(s, "ingest_kernel<u16>", 0.0, 0.0,
-                hipLaunchKernelGGL(ingest_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t *)src, Z, Y,
+                HCU_LAUNCH(ingest_kernel<uint16_t>, grid, dim3(256), 0, s, (const uint16_t *)src, Z, Y,
                                    X, C, nzt, nm, d));
       break;
     case HCU_U8:
       HCU_TIMED(s, "ingest_kernel<u8>", 0.0, 0.0,
-                hipLaunchKernelGGL(ingest_kernel<uint8_t>, grid, dim3(256), 0, s, (const uint8_t *)src, Z, Y,
+                HCU_LAUNCH(ingest_kernel<uint8_t>, grid, dim3(256), 0, s, (const uint8_t *)src, Z, Y,
                                    X, C, nzt, nm, d));
       break;
     case HCU_F64:
       HCU_TIMED(s, "ingest_kernel<f64>", 0.0, 0.0,
-                hipLaunchKernelGGL(ingest_kernel<double>, grid, dim3(256), 0, s, (const double *)src, Z, Y,
+                HCU_LAUNCH(ingest_kernel<double>, grid, dim3(256), 0, s, (const double *)src, Z, Y,
                                    X, C, nzt, nm, d));
       break;
     default:

@@ -118,7 +118,7 @@ int launch_s2b(const float *x, const float *sc, const float *sh, float *xs, int 
   const int NV = Cs * es / 16;
   const int64_t n = (int64_t)B * D[0] * D[1] * D[2] * S[0] * S[1] * S[2] * NV;
   HCU_TIMED(s, "s2b_kernel", 0.0, 16.0 * n * 2,
-            hipLaunchKernelGGL(s2b_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)x, sc, sh,
+            HCU_LAUNCH(s2b_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)x, sc, sh,
                                (uint4 *)xs, X, Y, Z, NV, D[0], D[1], D[2], S[0], S[1], S[2], n, es == 2));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -129,7 +129,7 @@ int launch_b2s(const float *ys, float *y, int B, int OX, int OY, int OZ, int Cs,
   const int NV = Cs * es / 16;
   const int64_t n = (int64_t)B * OX * OY * OZ * NV;
   HCU_TIMED(s, "b2s_kernel", 0.0, 16.0 * n * 2,
-            hipLaunchKernelGGL(b2s_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)ys, (uint4 *)y,
+            HCU_LAUNCH(b2s_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)ys, (uint4 *)y,
                                OX, OY, OZ, NV, D[0], D[1], D[2], S[0], S[1], S[2], n));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -140,7 +140,7 @@ int launch_crop_cl(const float *src, float *dst, int B, const int *sdims, const 
   const int NV = Cs * es / 16;
   const int64_t n = (int64_t)B * ddims[0] * ddims[1] * ddims[2] * NV;
   HCU_TIMED(s, "crop_kernel", 0.0, 16.0 * n * 2,
-            hipLaunchKernelGGL(crop_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)src,
+            HCU_LAUNCH(crop_kernel, dim3(layout_grid(n)), dim3(256), 0, s, (const uint4 *)src,
                                (uint4 *)dst, sdims[0], sdims[1], sdims[2], ddims[0], ddims[1], ddims[2], NV,
                                off[0], off[1], off[2], n));
   HCU_CHECK_LAUNCH();
@@ -231,11 +231,11 @@ int launch_from_cl_tiled(const float *y, const float *sc, const float *sh, float
   const double by = (double)B * V * (C * 4.0 + Cs * (bf ? 2.0 : 4.0));
   if (bf)
     HCU_TIMED(s, "from_cl_tile_kernel", 0.0, by,
-              hipLaunchKernelGGL(from_cl_tile_kernel<true>, grid, dim3(256), lds, s, (const void *)y, sc, sh,
+              HCU_LAUNCH(from_cl_tile_kernel<true>, grid, dim3(256), lds, s, (const void *)y, sc, sh,
                                  out, C, Cs, V));
   else
     HCU_TIMED(s, "from_cl_tile_kernel", 0.0, by,
-              hipLaunchKernelGGL(from_cl_tile_kernel<false>, grid, dim3(256), lds, s, (const void *)y, sc, sh,
+              HCU_LAUNCH(from_cl_tile_kernel<false>, grid, dim3(256), lds, s, (const void *)y, sc, sh,
                                  out, C, Cs, V));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -249,7 +249,7 @@ int launch_to_cl_tiled(const float *x, float *xcl, int B, int C, int Cs, int64_t
   const double by = (double)B * V * (C * (x_dtype == 0 ? 4.0 : 2.0) + Cs * (bf ? 2.0 : 4.0));
 #define TOCL(TI_, BF_)                                                                                    \
   HCU_TIMED(s, "to_cl_tile_kernel", 0.0, by,                                                             \
-            hipLaunchKernelGGL((to_cl_tile_kernel<TI_, BF_>), grid, dim3(256), lds, s, (const TI_ *)x,     \
+            HCU_LAUNCH((to_cl_tile_kernel<TI_, BF_>), grid, dim3(256), lds, s, (const TI_ *)x,     \
                                (void *)xcl, C, Cs, V))
   if (x_dtype == 0 && bf) TOCL(float, true);
   else if (x_dtype == 0) TOCL(float, false);
@@ -268,11 +268,11 @@ int launch_from_cl_act(const float *y, const float *sc, const float *sh, float *
   const int64_t n = (int64_t)B * C * V;
   if (bf)
     HCU_TIMED(s, "from_cl_act_kernel", 0.0, 6.0 * n,
-              hipLaunchKernelGGL(from_cl_act_kernel<true>, dim3(layout_grid(n)), dim3(256), 0, s, (const void *)y,
+              HCU_LAUNCH(from_cl_act_kernel<true>, dim3(layout_grid(n)), dim3(256), 0, s, (const void *)y,
                                  sc, sh, out, C, Cs, V, n));
   else
     HCU_TIMED(s, "from_cl_act_kernel", 0.0, 8.0 * n,
-              hipLaunchKernelGGL(from_cl_act_kernel<false>, dim3(layout_grid(n)), dim3(256), 0, s,
+              HCU_LAUNCH(from_cl_act_kernel<false>, dim3(layout_grid(n)), dim3(256), 0, s,
                                  (const void *)y, sc, sh, out, C, Cs, V, n));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -315,7 +315,7 @@ int hcu_gate_fwd(const float *hp, const float *zp, const float *hprev, float *ou
   if (!hp || !zp || !out || n < 0) return hcu::fail(1, "null argument");
   hipStream_t s = (hipStream_t)stream;
   HCU_TIMED(s, "gate_fwd_kernel", 0.0, 16.0 * n,
-            hipLaunchKernelGGL(hcu::gate_fwd_kernel, dim3(hcu::layout_grid(n)), dim3(256), 0, s, hp, zp, hprev,
+            HCU_LAUNCH(hcu::gate_fwd_kernel, dim3(hcu::layout_grid(n)), dim3(256), 0, s, hp, zp, hprev,
                                out, n));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -325,7 +325,7 @@ int hcu_gate_bwd(const float *hp, const float *zp, const float *hprev, const flo
   if (!hp || !zp || !dout || !dhp || !dzp || n < 0) return hcu::fail(1, "null argument");
   hipStream_t s = (hipStream_t)stream;
   HCU_TIMED(s, "gate_bwd_kernel", 0.0, 28.0 * n,
-            hipLaunchKernelGGL(hcu::gate_bwd_kernel, dim3(hcu::layout_grid(n)), dim3(256), 0, s, hp, zp, hprev,
+            HCU_LAUNCH(hcu::gate_bwd_kernel, dim3(hcu::layout_grid(n)), dim3(256), 0, s, hp, zp, hprev,
                                dout, dhp, dzp, dhprev, n));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -369,7 +369,7 @@ extern "C" int hcu_gather_vectors(float *const *vecs, const int *lens, int n, fl
   v.unpack = unpack != 0;
   hipStream_t s = (hipStream_t)stream;
   HCU_TIMED(s, "vec_gather_kernel", 0.0, 8.0 * v.off[n],
-            hipLaunchKernelGGL(hcu::vec_gather_kernel, dim3(n), dim3(256), 0, s, v, buf));
+            HCU_LAUNCH(hcu::vec_gather_kernel, dim3(n), dim3(256), 0, s, v, buf));
   HCU_CHECK_LAUNCH();
   return 0;
 }

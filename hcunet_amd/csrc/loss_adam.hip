@@ -92,11 +92,11 @@ int launch_loss_pixel(const float *pred, int B, int C, int PX, int PY, int PZ,
   const int64_t n = (int64_t)B * C * PX * PY * PZ;
   if (n <= 0) return fail(1, "loss: empty prediction");
   const int64_t chunk = (n + R - 1) / R;
-  HCU_TIMED(s, "loss_pixel_kernel", 0.0, 0.0, hipLaunchKernelGGL(loss_pixel_kernel, dim3(R), dim3(256), 0, s, pred, PX, PY, PZ, mask,
+  HCU_TIMED(s, "loss_pixel_kernel", 0.0, 0.0, HCU_LAUNCH(loss_pixel_kernel, dim3(R), dim3(256), 0, s, pred, PX, PY, PZ, mask,
                      mask_dtype, pwl, pwl_dtype, MX, MY, MZ, dpred, part, n, chunk,
                      1.f / (float)n));
   HCU_CHECK_LAUNCH();
-  HCU_TIMED(s, "loss_finalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, R, (double)n, loss));
+  HCU_TIMED(s, "loss_finalize_kernel", 0.0, 0.0, HCU_LAUNCH(loss_finalize_kernel, dim3(1), dim3(256), 0, s, part, R, (double)n, loss));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -111,7 +111,7 @@ scale_kernel(const float *src, const float *scale, float *dst, int64_t n) {
 
 int launch_scale(const float *src, const float *scale, float *dst, int64_t n, hipStream_t s) {
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-  HCU_TIMED(s, "scale_kernel", 0.0, 0.0, hipLaunchKernelGGL(scale_kernel, dim3(blocks), dim3(256), 0, s, src, scale, dst, n));
+  HCU_TIMED(s, "scale_kernel", 0.0, 0.0, HCU_LAUNCH(scale_kernel, dim3(blocks), dim3(256), 0, s, src, scale, dst, n));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -147,7 +147,7 @@ int launch_adam(float *p, const float *g, float *m, float *v, int64_t n, float l
   const float neg_step = (float)(-(double)lr / bc1);
   const float bc2s = (float)std::sqrt(bc2);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4096));
-  HCU_TIMED(s, "adam_kernel", 0.0, 0.0, hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n, b1, b2, eps,
+  HCU_TIMED(s, "adam_kernel", 0.0, 0.0, HCU_LAUNCH(adam_kernel, dim3(blocks), dim3(256), 0, s, p, g, m, v, n, b1, b2, eps,
                      wd, neg_step, bc2s, grad_scale));
   HCU_CHECK_LAUNCH();
   return 0;

@@ -376,10 +376,10 @@ int hcu_loss_ext_fwd(int mode, const float *pred, int B, int C, int PX, int PY, 
     const int R = lx_rows(nrows);
     const int64_t chunk = (nrows + R - 1) / R;
     HCU_TIMED(s, "loss_ext_fwd_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL(loss_ext_fwd_kernel, dim3(R, PZ), dim3(256), 0, s, g, mode, part, chunk));
+              HCU_LAUNCH(loss_ext_fwd_kernel, dim3(R, PZ), dim3(256), 0, s, g, mode, part, chunk));
     HCU_CHECK_LAUNCH();
     HCU_TIMED(s, "loss_ext_finalize_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL(loss_ext_finalize_kernel, dim3(1), dim3(256), 0, s, part, R, PZ, mode,
+              HCU_LAUNCH(loss_ext_finalize_kernel, dim3(1), dim3(256), 0, s, part, R, PZ, mode,
                                  (double)g.n, (double)PX * PY, zscale, loss, aux));
     HCU_CHECK_LAUNCH();
     return 0;
@@ -387,10 +387,10 @@ int hcu_loss_ext_fwd(int mode, const float *pred, int B, int C, int PX, int PY, 
   const int R = lx_rows(g.n);
   const int64_t chunk = (g.n + R - 1) / R;
   HCU_TIMED(s, "loss_ext_fwd_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_ext_fwd_kernel, dim3(R), dim3(256), 0, s, g, mode, part, chunk));
+            HCU_LAUNCH(loss_ext_fwd_kernel, dim3(R), dim3(256), 0, s, g, mode, part, chunk));
   HCU_CHECK_LAUNCH();
   HCU_TIMED(s, "loss_ext_finalize_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_ext_finalize_kernel, dim3(1), dim3(256), 0, s, part, R, 0, mode,
+            HCU_LAUNCH(loss_ext_finalize_kernel, dim3(1), dim3(256), 0, s, part, R, 0, mode,
                                (double)g.n, (double)PX * PY, zscale, loss, aux));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -407,7 +407,7 @@ int hcu_loss_ext_bwd(int mode, const float *pred, int B, int C, int PX, int PY, 
   hipStream_t s = (hipStream_t)stream;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((g.n + 255) / 256, 4096));
   HCU_TIMED(s, "loss_ext_bwd_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_ext_bwd_kernel, dim3(blocks), dim3(256), 0, s, g, mode, aux, counts,
+            HCU_LAUNCH(loss_ext_bwd_kernel, dim3(blocks), dim3(256), 0, s, g, mode, aux, counts,
                                grad_out, dpred));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -424,7 +424,7 @@ int hcu_loss_random_count(const float *pred, int B, int C, int PX, int PY, int P
   const int R = lx_rows(g.n);
   const int64_t chunk = (g.n + R - 1) / R;
   HCU_TIMED(s, "loss_random_count_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_random_count_kernel, dim3(R), dim3(256), 0, s, g, chunk, counts));
+            HCU_LAUNCH(loss_random_count_kernel, dim3(R), dim3(256), 0, s, g, chunk, counts));
   HCU_CHECK_LAUNCH();
   return 0;
 }
@@ -444,16 +444,16 @@ int hcu_loss_random_fwd(const float *pred, int B, int C, int PX, int PY, int PZ,
   const int R = lx_rows(g.n);
   const int64_t chunk = (g.n + R - 1) / R;
   HCU_TIMED(s, "loss_random_compact_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_random_compact_kernel, dim3(R), dim3(256), 0, s, g, chunk, offsets,
+            HCU_LAUNCH(loss_random_compact_kernel, dim3(R), dim3(256), 0, s, g, chunk, offsets,
                                pos_list, neg_list));
   HCU_CHECK_LAUNCH();
   double *part = (double *)scratch;
   HCU_TIMED(s, "loss_random_gather_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_random_gather_kernel, dim3(RG), dim3(256), 0, s, g, pos_list, neg_list,
+            HCU_LAUNCH(loss_random_gather_kernel, dim3(RG), dim3(256), 0, s, g, pos_list, neg_list,
                                pos_ind, neg_ind, n, counts, part));
   HCU_CHECK_LAUNCH();
   HCU_TIMED(s, "loss_ext_finalize_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(loss_ext_finalize_kernel, dim3(1), dim3(256), 0, s, part, RG, 0,
+            HCU_LAUNCH(loss_ext_finalize_kernel, dim3(1), dim3(256), 0, s, part, RG, 0,
                                (int)LM_RANDOM, 2.0 * n, 1.0, (const float *)nullptr, loss, aux));
   HCU_CHECK_LAUNCH();
   return 0;

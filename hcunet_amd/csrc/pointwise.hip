@@ -44,10 +44,10 @@ __device__ __forceinline__ void st1(bf16_t *p, float v) { p->v = f2bf(v); }
   do {                                                       \
     if (bf) {                                                \
       using T = bf16_t;                                      \
-      hipLaunchKernelGGL(KERNEL<T>, __VA_ARGS__);            \
+      HCU_LAUNCH(KERNEL<T>, __VA_ARGS__);            \
     } else {                                                 \
       using T = float;                                       \
-      hipLaunchKernelGGL(KERNEL<T>, __VA_ARGS__);            \
+      HCU_LAUNCH(KERNEL<T>, __VA_ARGS__);            \
     }                                                        \
   } while (0)
 __device__ __forceinline__ float comp(const float4 &v, int j) {
@@ -173,7 +173,7 @@ int launch_bn_fwd_finalize(const float *stats, int R, int statsW, int C, int Cs,
                            float *run_mean, float *run_var, int64_t *nbt,
                            float eps, float momentum, int training, BNCoef coef,
                            hipStream_t s) {
-  HCU_TIMED(s, "bn_fwd_finalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, stats, R,
+  HCU_TIMED(s, "bn_fwd_finalize_kernel", 0.0, 0.0, HCU_LAUNCH(bn_fwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, stats, R,
                      statsW, C, count, gamma, beta, run_mean, run_var, nbt, eps,
                      momentum, training, coef));
   HCU_CHECK_LAUNCH();
@@ -229,7 +229,7 @@ bn_bwd_finalize_kernel(const float *part, int R, int C, int W, double count,
 int launch_bn_bwd_finalize(const float *part, int R, int C, int Cs, int W, double count,
                            BNCoef coef, float *dgamma, float *dbeta, int training,
                            int accumulate, hipStream_t s) {
-  HCU_TIMED(s, "bn_bwd_finalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, part, R, C,
+  HCU_TIMED(s, "bn_bwd_finalize_kernel", 0.0, 0.0, HCU_LAUNCH(bn_bwd_finalize_kernel, dim3(Cs), dim3(256), 0, s, part, R, C,
                      W, count, coef, dgamma, dbeta, training, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1112,7 +1112,7 @@ reduce_partials_kernel(const float *part, int R, int W, float *out, int accumula
 
 int launch_reduce_partials(const float *part, int R, int W, int n, float *out,
                            int accumulate, hipStream_t s) {
-  HCU_TIMED(s, "reduce_partials_kernel", 0.0, 0.0, hipLaunchKernelGGL(reduce_partials_kernel, dim3(n), dim3(256), 0, s, part, R,
+  HCU_TIMED(s, "reduce_partials_kernel", 0.0, 0.0, HCU_LAUNCH(reduce_partials_kernel, dim3(n), dim3(256), 0, s, part, R,
                      W, out, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1164,23 +1164,23 @@ int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hi
     const dim3 g2((nv + 255) / 256);
     if (x_dtype == 1 && bf)
       HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
-                hipLaunchKernelGGL((to_cl_vox_kernel<_Float16, bf16_t>), g2, dim3(256), 0, s,
+                HCU_LAUNCH((to_cl_vox_kernel<_Float16, bf16_t>), g2, dim3(256), 0, s,
                                    (const _Float16 *)x, (bf16_t *)xcl, C, V, nv, fV));
     else if (x_dtype == 3 && bf)
       HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
-                hipLaunchKernelGGL((to_cl_vox_kernel<bf16_t, bf16_t>), g2, dim3(256), 0, s,
+                HCU_LAUNCH((to_cl_vox_kernel<bf16_t, bf16_t>), g2, dim3(256), 0, s,
                                    (const bf16_t *)x, (bf16_t *)xcl, C, V, nv, fV));
     else if (x_dtype == 0 && bf)
       HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
-                hipLaunchKernelGGL((to_cl_vox_kernel<float, bf16_t>), g2, dim3(256), 0, s, x,
+                HCU_LAUNCH((to_cl_vox_kernel<float, bf16_t>), g2, dim3(256), 0, s, x,
                                    (bf16_t *)xcl, C, V, nv, fV));
     else if (x_dtype == 1)
       HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
-                hipLaunchKernelGGL((to_cl_vox_kernel<_Float16, float>), g2, dim3(256), 0, s,
+                HCU_LAUNCH((to_cl_vox_kernel<_Float16, float>), g2, dim3(256), 0, s,
                                    (const _Float16 *)x, xcl, C, V, nv, fV));
     else if (x_dtype == 0)
       HCU_TIMED(s, "to_cl_vox_kernel", 0.0, 0.0,
-                hipLaunchKernelGGL((to_cl_vox_kernel<float, float>), g2, dim3(256), 0, s, x, xcl, C, V,
+                HCU_LAUNCH((to_cl_vox_kernel<float, float>), g2, dim3(256), 0, s, x, xcl, C, V,
                                    nv, fV));
     else
       return fail(4, "to_cl: unsupported input dtype");
@@ -1190,23 +1190,23 @@ int launch_to_cl(const float *x, float *xcl, int B, int C, int Cs, int64_t V, hi
   if (launch_to_cl_tiled(x, xcl, B, C, Cs, V, s, bf, x_dtype) == 0) return 0;
   if (x_dtype == 1 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL((to_cl_kernel<_Float16, bf16_t>), gr, dim3(256), 0, s,
+              HCU_LAUNCH((to_cl_kernel<_Float16, bf16_t>), gr, dim3(256), 0, s,
                                  (const _Float16 *)x, (bf16_t *)xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 3 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL((to_cl_kernel<bf16_t, bf16_t>), gr, dim3(256), 0, s,
+              HCU_LAUNCH((to_cl_kernel<bf16_t, bf16_t>), gr, dim3(256), 0, s,
                                  (const bf16_t *)x, (bf16_t *)xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 0 && bf)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL((to_cl_kernel<float, bf16_t>), gr, dim3(256), 0, s, x,
+              HCU_LAUNCH((to_cl_kernel<float, bf16_t>), gr, dim3(256), 0, s, x,
                                  (bf16_t *)xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 1)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL((to_cl_kernel<_Float16, float>), gr, dim3(256), 0, s,
+              HCU_LAUNCH((to_cl_kernel<_Float16, float>), gr, dim3(256), 0, s,
                                  (const _Float16 *)x, xcl, B, C, Cs, V, fV, fC4));
   else if (x_dtype == 0)
     HCU_TIMED(s, "to_cl_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL((to_cl_kernel<float, float>), gr, dim3(256), 0, s, x, xcl, B, C,
+              HCU_LAUNCH((to_cl_kernel<float, float>), gr, dim3(256), 0, s, x, xcl, B, C,
                                  Cs, V, fV, fC4));
   else
     return fail(4, "to_cl: unsupported input dtype");
@@ -1285,7 +1285,7 @@ int launch_prep_conv_fwd(const float *w, float *wg, int Cout, int Cin_g, int gro
                          int fold_mod, int T, int ECs, int CoutW, WPack pk, hipStream_t s) {
   const int E = std::min(fold_mod, groups * Cin_g);
   const int64_t n = wpack_count(pk, T, ECs, CoutW);
-  HCU_TIMED(s, "prep_conv_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
+  HCU_TIMED(s, "prep_conv_fwd_kernel", 0.0, 0.0, HCU_LAUNCH(prep_conv_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
                      Cin_g, groups, fold_mod, T, ECs, CoutW, E, pk));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1309,7 +1309,7 @@ prep_conv_dgrad_kernel(const float *w, float *wg, int Cout, int Cin_g, int group
 int launch_prep_conv_dgrad(const float *w, float *wg, int Cout, int Cin_g, int groups,
                            int fold_mod, int T, int OCs, int EW, int E, WPack pk, hipStream_t s) {
   const int64_t n = wpack_count(pk, T, OCs, EW);
-  HCU_TIMED(s, "prep_conv_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
+  HCU_TIMED(s, "prep_conv_dgrad_kernel", 0.0, 0.0, HCU_LAUNCH(prep_conv_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cout,
                      Cin_g, groups, fold_mod, T, OCs, EW, E, pk));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1341,7 +1341,7 @@ int launch_prep_convt_fwd(const float *w, float *wg, int Cin, int Cout, int KX, 
                           int KZ, int sx, int sy, int sz, int px, int py, int pz, int Jx,
                           int Jy, int Jz, int ICs, int CoutW, hipStream_t s) {
   const int64_t n = (int64_t)Jx * Jy * Jz * ICs * CoutW;
-  HCU_TIMED(s, "prep_convt_fwd_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_convt_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
+  HCU_TIMED(s, "prep_convt_fwd_kernel", 0.0, 0.0, HCU_LAUNCH(prep_convt_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
                      Cout, KX, KY, KZ, sx, sy, sz, px, py, pz, Jx, Jy, Jz, ICs, CoutW));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1376,7 +1376,7 @@ int launch_prep_convt_fused(const float *w, float *wg, int Cin, int Cout, int KX
   const int T = (KX / sx) * (KY / sy) * (KZ / sz);
   const int64_t n = wpack_count(pk, T, ICs, CoutW);
   HCU_TIMED(s, "prep_convt_fused_kernel", 0.0, 0.0,
-            hipLaunchKernelGGL(prep_convt_fused_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg,
+            HCU_LAUNCH(prep_convt_fused_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg,
                                Cin, Cout, KX, KY, KZ, sx, sy, sz, ICs, CoutW, pk));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1399,7 +1399,7 @@ prep_convt_dgrad_kernel(const float *w, float *wg, int Cin, int Cout, int T, int
 int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T, int UCs,
                             int CinW, WPack pk, hipStream_t s) {
   const int64_t n = wpack_count(pk, T, UCs, CinW);
-  HCU_TIMED(s, "prep_convt_dgrad_kernel", 0.0, 0.0, hipLaunchKernelGGL(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
+  HCU_TIMED(s, "prep_convt_dgrad_kernel", 0.0, 0.0, HCU_LAUNCH(prep_convt_dgrad_kernel, dim3(grid_for(n)), dim3(256), 0, s, w, wg, Cin,
                      Cout, T, UCs, CinW, pk));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1429,7 +1429,7 @@ outconv_wfinalize_kernel(const float *part, int R, int Co, int C, int Cs, float 
 int launch_outconv_wfinalize(const float *part_oc, int R, int Co, int C, int Cs, float *dw,
                              float *db, int accumulate, hipStream_t s) {
   const int n = Co * C + Co;
-  HCU_TIMED(s, "outconv_wfinalize_kernel", 0.0, 0.0, hipLaunchKernelGGL(outconv_wfinalize_kernel, dim3(n), dim3(256), 0, s, part_oc,
+  HCU_TIMED(s, "outconv_wfinalize_kernel", 0.0, 0.0, HCU_LAUNCH(outconv_wfinalize_kernel, dim3(n), dim3(256), 0, s, part_oc,
                      R, Co, C, Cs, dw, db, accumulate));
   HCU_CHECK_LAUNCH();
   return 0;
@@ -1450,7 +1450,7 @@ int launch_bn_count_increment(int64_t *const *ptrs, int n, hipStream_t s) {
   CountPtrs c{};
   for (int i = 0; i < n; ++i) c.p[i] = ptrs[i];
   c.n = n;
-  HCU_TIMED(s, "bn_count_kernel", 0.0, 0.0, hipLaunchKernelGGL(bn_count_kernel, dim3(1), dim3(64), 0, s, c));
+  HCU_TIMED(s, "bn_count_kernel", 0.0, 0.0, HCU_LAUNCH(bn_count_kernel, dim3(1), dim3(64), 0, s, c));
   HCU_CHECK_LAUNCH();
   return 0;
 }

@@ -162,7 +162,7 @@ int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, i
     // enough workgroups that the largest job is ~8 elements per thread
     const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((most + 2047) / 2048, 1024));
     HCU_TIMED(s, "prep_all_kernel", 0.0, 0.0,
-              hipLaunchKernelGGL(prep_all_kernel, dim3(gx, b.n), dim3(256), 0, s, params,
+              HCU_LAUNCH(prep_all_kernel, dim3(gx, b.n), dim3(256), 0, s, params,
                                  dst_base, b));
     HCU_CHECK_LAUNCH();
   }

@@ -128,12 +128,12 @@ extern "C" int hcu_tile_gather(const void *image, int image_dtype, int C, int X,
   const double bytes = (double)n * 4.0 * 2.0;
   if (image_dtype == HCU_F32)
     HCU_TIMED(s, "tile_gather_kernel", 0.0, bytes,
-              hipLaunchKernelGGL((tile_gather_kernel<float>), dim3(g), dim3(256), 0, s,
+              HCU_LAUNCH((tile_gather_kernel<float>), dim3(g), dim3(256), 0, s,
                                  (const float *)image, C, X, Y, Z, pads[0], pads[1], pads[2],
                                  tile_dims[0], tile_dims[1], tile_dims[2], tb, clean, out));
   else if (image_dtype == HCU_F16)
     HCU_TIMED(s, "tile_gather_kernel", 0.0, bytes,
-              hipLaunchKernelGGL((tile_gather_kernel<_Float16>), dim3(g), dim3(256), 0, s,
+              HCU_LAUNCH((tile_gather_kernel<_Float16>), dim3(g), dim3(256), 0, s,
                                  (const _Float16 *)image, C, X, Y, Z, pads[0], pads[1], pads[2],
                                  tile_dims[0], tile_dims[1], tile_dims[2], tb, clean, out));
   else
@@ -162,7 +162,7 @@ extern "C" int hcu_tile_scatter(const float *out, const int *out_dims, const int
   const double bytes = (double)n * (4.0 + (mask_dtype == HCU_U8 ? 1.0 : 4.0));
   if (mask_dtype == HCU_U8)
     HCU_TIMED(s, "tile_scatter_kernel", 0.0, bytes,
-              hipLaunchKernelGGL((tile_scatter_kernel<uint8_t>), dim3(g), dim3(256), 0, s, out,
+              HCU_LAUNCH((tile_scatter_kernel<uint8_t>), dim3(g), dim3(256), 0, s, out,
                                  out_dims[0], out_dims[1], out_dims[2], crop_lo[0], crop_lo[1],
                                  crop_lo[2], bcast[0], bcast[1], bcast[2], (uint8_t *)mask,
                                  mask_dims[0], mask_dims[1], mask_dims[2], dst_lo[0], dst_lo[1],
@@ -170,7 +170,7 @@ extern "C" int hcu_tile_scatter(const float *out, const int *out_dims, const int
                                  threshold ? 1 : 0, thr));
   else if (mask_dtype == HCU_F32)
     HCU_TIMED(s, "tile_scatter_kernel", 0.0, bytes,
-              hipLaunchKernelGGL((tile_scatter_kernel<float>), dim3(g), dim3(256), 0, s, out,
+              HCU_LAUNCH((tile_scatter_kernel<float>), dim3(g), dim3(256), 0, s, out,
                                  out_dims[0], out_dims[1], out_dims[2], crop_lo[0], crop_lo[1],
                                  crop_lo[2], bcast[0], bcast[1], bcast[2], (float *)mask,
                                  mask_dims[0], mask_dims[1], mask_dims[2], dst_lo[0], dst_lo[1],

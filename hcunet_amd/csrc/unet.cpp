@@ -507,18 +507,19 @@ struct hcu_unet_plan {
   mutable hipStream_t side = nullptr;
   mutable int side_device = -1;
   mutable hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_slot[HCU_NBUF] = {};
+  mutable hipEvent_t ev_chain = nullptr;   // stop event of the chain's kernels (Ctx::arm_chain)
   // data-parallel overlap (hcu_unet_set_grad_events): caller-owned events the
   // backward records when the decoder's / the deep encoder levels' gradients are final
   hipEvent_t grad_ev[2] = {nullptr, nullptr};
   int grad_deep = -1;
   void destroy_side() const {
     if (side) (void)hipStreamDestroy(side);
-    for (hipEvent_t *e : {&ev_fork, &ev_join})
+    for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_chain})
       if (*e) (void)hipEventDestroy(*e);
     for (hipEvent_t &e : ev_slot)
       if (e) (void)hipEventDestroy(e);
     side = nullptr;
-    ev_fork = ev_join = nullptr;
+    ev_fork = ev_join = ev_chain = nullptr;
     for (hipEvent_t &e : ev_slot) e = nullptr;
   }
   ~hcu_unet_plan() {
@@ -865,9 +866,39 @@ struct Ctx {
   // Branch work issued from here on sees everything the main chain has issued.
   int fork() {
     if (!split) return HCU_OK;
+    // HCU_FORK_DUP=N (measurement): N extra markers on the chain per fork
+    static const int dup = getenv("HCU_FORK_DUP") ? atoi(getenv("HCU_FORK_DUP")) : 0;
+    for (int k = 0; k < dup; ++k) HCU_HIP(hipEventRecord(p.ev_fork, s));
+    const ChainRec &r = chain_rec();
+    if (r.ev == p.ev_chain && r.s == s && r.n > chain_n0) {
+      // the chain's last kernel carries ev_chain as its stop event (HCU_LAUNCH)
+      HCU_HIP(hipStreamWaitEvent(ws, p.ev_chain, 0));
+      return HCU_OK;
+    }
     HCU_HIP(hipEventRecord(p.ev_fork, s));
     HCU_HIP(hipStreamWaitEvent(ws, p.ev_fork, 0));
     return HCU_OK;
+  }
+  // Arms the chain record (backward): kernels launched on s from here on
+  // carry ev_chain, so forks need no marker; disarmed by the destructor.
+  unsigned long chain_n0 = 0;
+  bool armed = false;
+  void arm_chain() {
+    static const bool off = getenv("HCU_FORK_MARKERS") && getenv("HCU_FORK_MARKERS")[0] == '1';   // A/B
+    if (!split || off || !p.ev_chain) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // captured graphs keep their markers
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+      (void)hipGetLastError();
+      return;
+    }
+    ChainRec &r = chain_rec();
+    r.s = s;
+    r.ev = p.ev_chain;
+    chain_n0 = r.n;
+    armed = true;
+  }
+  ~Ctx() {
+    if (armed) chain_rec().ev = nullptr;
   }
   // The branch work issued so far is the last reader of `slot`.
   int read_done(int slot) {
@@ -1413,6 +1444,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   c.split = split;
   c.ws = split ? p.side : c.s;
+  c.arm_chain();
   // an eval-mode forward prepared only the forward weight images: the
   // input-gradient images are laid out here
   if (!training && !p.prep_bwd.empty())
@@ -1593,7 +1625,7 @@ int ensure_side(const hcu_unet_plan &p, int dev) {
   p.destroy_side();
   HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
   p.side_device = dev;
-  for (hipEvent_t *e : {&p.ev_fork, &p.ev_join})
+  for (hipEvent_t *e : {&p.ev_fork, &p.ev_join, &p.ev_chain})
     HCU_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (hipEvent_t &e : p.ev_slot) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return HCU_OK;

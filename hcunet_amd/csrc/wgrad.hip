@@ -643,7 +643,7 @@ int launch_wgrad(const WGradArgs &a, hipStream_t s) {
 #define W2(NS_, MS_)                                                                       \
   if (!ok && a.NS == NS_ && a.MS == MS_) {                                                 \
     HCU_TIMED(s, "wgrad2_kernel<" #NS_ "," #MS_ ">", fl2, by2,                              \
-              hipLaunchKernelGGL((wgrad2_kernel<NS_, MS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+              HCU_LAUNCH((wgrad2_kernel<NS_, MS_>), grid, dim3(256), a.lds_bytes, s, a)); \
     ok = true;                                                                             \
   }
     W2(1, 1) W2(1, 2) W2(1, 3) W2(1, 4) W2(1, 5) W2(1, 6) W2(1, 7) W2(1, 8)
@@ -662,13 +662,13 @@ int launch_wgrad(const WGradArgs &a, hipStream_t s) {
                            (double)wgrad_partial_floats(a));
   if (a.NS == 4) {
     HCU_TIMED(s, "wgrad_kernel<4,4>", fl, by,
-              hipLaunchKernelGGL((wgrad_kernel<4, 4>), grid, dim3(256), a.lds_bytes, s, a));
+              HCU_LAUNCH((wgrad_kernel<4, 4>), grid, dim3(256), a.lds_bytes, s, a));
   } else if (a.NS == 2) {
     HCU_TIMED(s, "wgrad_kernel<2,8>", fl, by,
-              hipLaunchKernelGGL((wgrad_kernel<2, 8>), grid, dim3(256), a.lds_bytes, s, a));
+              HCU_LAUNCH((wgrad_kernel<2, 8>), grid, dim3(256), a.lds_bytes, s, a));
   } else {
     HCU_TIMED(s, "wgrad_kernel<1,16>", fl, by,
-              hipLaunchKernelGGL((wgrad_kernel<1, 16>), grid, dim3(256), a.lds_bytes, s, a));
+              HCU_LAUNCH((wgrad_kernel<1, 16>), grid, dim3(256), a.lds_bytes, s, a));
   }
   HCU_CHECK_LAUNCH();
   return 0;
@@ -766,7 +766,7 @@ int launch_wgrad_finalize_batch(const WGradFinalize *fs, int n, hipStream_t s) {
       by += 4.0 * (double)b.f[k].Mtot * b.f[k].Ntot * (b.f[k].KB + 1);
     }
     HCU_TIMED(s, "wgrad_finalize_batch_kernel", 0.0, by,
-              hipLaunchKernelGGL(wgrad_finalize_batch_kernel, dim3(gx, b.n), dim3(256), 0, s, b));
+              HCU_LAUNCH(wgrad_finalize_batch_kernel, dim3(gx, b.n), dim3(256), 0, s, b));
     HCU_CHECK_LAUNCH();
   }
   return 0;
@@ -777,7 +777,7 @@ int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s) {
   int S, blocks;
   wgf_geometry(f, S, blocks);
   HCU_TIMED(s, "wgrad_finalize_kernel", 0.0, 4.0 * (double)n * (f.KB + 1),
-            hipLaunchKernelGGL(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f, S));
+            HCU_LAUNCH(wgrad_finalize_kernel, dim3(blocks), dim3(256), 0, s, f, S));
   HCU_CHECK_LAUNCH();
   return 0;
 }

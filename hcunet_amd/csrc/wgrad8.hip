@@ -581,10 +581,10 @@ int launch_wgrad8(const WGradArgs &a, hipStream_t s) {
   if (!ok && a.w8mode == MODE_ && a.MS == NR_) {                                                          \
     if (a.g_y)                                                                                            \
       HCU_TIMED(s, "wgrad8_kernel<" #MODE_ "," #NR_ ",gap>", fl, by,                                      \
-                hipLaunchKernelGGL((wgrad8_kernel<MODE_, NR_, true>), grid, dim3(256), a.lds_bytes, s, a)); \
+                HCU_LAUNCH((wgrad8_kernel<MODE_, NR_, true>), grid, dim3(256), a.lds_bytes, s, a)); \
     else                                                                                                  \
       HCU_TIMED(s, "wgrad8_kernel<" #MODE_ "," #NR_ ">", fl, by,                                          \
-                hipLaunchKernelGGL((wgrad8_kernel<MODE_, NR_, false>), grid, dim3(256), a.lds_bytes, s, a)); \
+                HCU_LAUNCH((wgrad8_kernel<MODE_, NR_, false>), grid, dim3(256), a.lds_bytes, s, a)); \
     ok = true;                                                                                            \
   }
   W8(0, 1) W8(0, 2) W8(0, 3) W8(0, 4) W8(0, 5) W8(0, 6) W8(0, 7) W8(0, 8)
@@ -592,7 +592,7 @@ int launch_wgrad8(const WGradArgs &a, hipStream_t s) {
 #define W8Q(NRW_)                                                                             \
   if (!ok && a.w8mode == 1 && cdiv(a.MS, a.w8nh) == NRW_) {                                   \
     HCU_TIMED(s, "wgrad8_kernel<1," #NRW_ ">", fl, by,                                        \
-              hipLaunchKernelGGL((wgrad8_kernel<1, NRW_, false>), grid, dim3(256), a.lds_bytes, s, a)); \
+              HCU_LAUNCH((wgrad8_kernel<1, NRW_, false>), grid, dim3(256), a.lds_bytes, s, a)); \
     ok = true;                                                                                \
   }
   W8Q(2) W8Q(3) W8Q(4) W8Q(5) W8Q(6) W8Q(7) W8Q(8) W8Q(9) W8Q(10)
