@@ -919,6 +919,11 @@ void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
 }
 
+bool bnfin_enabled() {
+  static const bool on = getenv("HCU_BNFIN") && getenv("HCU_BNFIN")[0] == '1';
+  return on;
+}
+
 int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float *isc,
                  const float *ish, int training) {
   HCU_HIP(hipGetLastError());
@@ -937,8 +942,7 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   // last workgroup.  Measured slower (+35..60 us per layer on MI355X: every
   // workgroup's agent-scope release fence writes back its XCD's L2), so the
   // separate finalize launch stays the default.
-  static const bool use_fin = getenv("HCU_BNFIN") && getenv("HCU_BNFIN")[0] == '1';
-  if (training && a.use_bconv && use_fin && a.lds_bytes - (int)sizeof(GConvArgs) >= 6144) {
+  if (training && a.use_bconv && bnfin_enabled() && a.lds_bytes - (int)sizeof(GConvArgs) >= 6144) {
     BnFin &f = a.fin;
     f.gamma = c.P + L.bn.gamma;
     f.beta = c.P + L.bn.beta;
@@ -1307,7 +1311,9 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   c.ws = split ? p.side : c.s;
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
-  if (training) HCU_HIP(hipMemsetAsync(c.fptr(c.sc, p.fin_off), 0, 64, c.s));
+  // the fused-finalize ticket counters (HCU_BNFIN) start from 0: a memset only then
+  // (a packet on the chain costs ~3 us of GPU time)
+  if (training && bnfin_enabled()) HCU_HIP(hipMemsetAsync(c.fptr(c.sc, p.fin_off), 0, 64, c.s));
   tag(std::string("in"), "fwd");
   if (!input_done)
     if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
