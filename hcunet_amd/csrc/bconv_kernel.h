@@ -219,20 +219,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // first stored channel of the block (ConvTranspose3d phases: all NT columns
   // of a block belong to one phase, the planner requires Cout % NT == 0)
   const int co0 = a.nph > 1 ? n0 - (n0 / a.Cout) * a.Cout : n0;
-  for (int j = tid; j < NT; j += 256) {
-    const int c = co0 + j;
-    coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
-    const bool bn = BNB && !split && c < a.OCs;
-    coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;
-    coefL[2 * NT + j] = bn ? a.bn_shift[c] : 0.f;
-    coefL[3 * NT + j] = bn ? a.bn_mean[c] : 0.f;
-    coefL[4 * NT + j] = bn ? a.bn_invstd[c] : 0.f;
-  }
-  if (a.in_scale)
-    for (int c = tid; c < a.ICs; c += 256) {
-      actL[c] = a.in_scale[c];
-      actL[a.ICs + c] = a.in_shift[c];
-    }
+  // (the coefficient loads follow the first halo fetch: load_coefs below)
 
   auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
     int r, tzi, tyi, txi;
@@ -334,6 +321,53 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
+  };
+  // The block's first halo fetch, from the kernel arguments themselves (the
+  // LDS copy is not written yet): issued before the coefficient loads and the
+  // weight staging, so their global round trips overlap instead of adding up
+  // (a one-tile block of a deep level spent ~6 K cycles in its prologue).
+  auto fetch_first = [&](int tile, int chunk) {
+    int b, r, tzi, tyi, txi;
+    a.fNT.divmod(tile, b, r);
+    a.fNTZ.divmod(r, r, tzi);
+    a.fNTY.divmod(r, txi, tyi);
+    const int x0 = txi * a.TX, y0 = tyi * a.TY, z0 = tzi * a.TZ;
+    const int IX = a.IX, IY = a.IY, IZ = a.IZ, ICs = a.ICs;
+    const uint32_t bZ = (uint32_t)ICs * ES, bY = (uint32_t)IZ * bZ, bX = (uint32_t)IY * bY;
+    const int gx0 = x0 * a.sx - a.px, gy0 = y0 * a.sy - a.py, gz0 = z0 * a.sz - a.pz;
+    const char *bp = reinterpret_cast<const char *>(a.in) + (size_t)b * IX * bX;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, IX * (int)bX, 0x00020000);
+    const int base_off = gx0 * (int)bX + gy0 * (int)bY + gz0 * (int)bZ + (chunk * CK + cv * VEC) * ES;
+    okbits = 0;
+#pragma unroll
+    for (int u = 0; u < NPFR; ++u) {
+      const int hp = hpk[u];
+      const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
+      const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
+      const bool ok = (hp >= 0) & ((unsigned)gx < (unsigned)IX) & ((unsigned)gy < (unsigned)IY) &
+                      ((unsigned)gz < (unsigned)IZ);
+      const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
+                         : 0x7ffffff0;
+      pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      okbits |= (uint32_t)ok << u;
+    }
+  };
+  auto load_coefs = [&]() {
+    for (int j = tid; j < NT; j += 256) {
+      const int c = co0 + j;
+      coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
+      const bool bn = BNB && !split && c < a.OCs;
+      coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;
+      coefL[2 * NT + j] = bn ? a.bn_shift[c] : 0.f;
+      coefL[3 * NT + j] = bn ? a.bn_mean[c] : 0.f;
+      coefL[4 * NT + j] = bn ? a.bn_invstd[c] : 0.f;
+    }
+    if (a.in_scale)
+      for (int c = tid; c < a.ICs; c += 256) {
+        actL[c] = a.in_scale[c];
+        actL[a.ICs + c] = a.in_shift[c];
+      }
   };
   // BatchNorm+ReLU of VEC channels, 0 outside the input
   auto activate = [&](uint4 v, bool ok, int chunk) -> uint4 {
@@ -529,11 +563,13 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     for (int k = 0; k < MPW * NSUB; ++k) __builtin_amdgcn_raw_buffer_store_b64(z, zr, 32 * k, 0, 0);
   };
 
-  lds_barrier();   // sa, tables and coefficients are in LDS
   // ---- main loop over (tile, chunk) items; contiguous tile range per block:
   // consecutive tiles share halo rows, which then come from this CU's L2
   const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
   const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
+  if (NPF > 0 && t_beg < t_end) fetch_first(t_beg, cb);
+  load_coefs();
+  lds_barrier();   // sa, tables and coefficients are in LDS
 #ifdef HCU_BCONV_PHASES
   long long ph_acc[6] = {0, 0, 0, 0, 0, 0};
   long long ph_t = (long long)__builtin_readcyclecounter();
@@ -542,10 +578,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   if (NPF > 0) {
     int tile = t_beg;
     if (nck == 1) stage_w(cb);
-    if (tile < t_end) {
-      fetch(tile, cb);
-      if (wpre) wfetch(cb);
-    }
+    if (tile < t_end && wpre) wfetch(cb);   // the halo of (t_beg, cb) is in flight (fetch_first)
     dummy_epilogue();
     for (; tile < t_end; ++tile) {
 #pragma unroll
