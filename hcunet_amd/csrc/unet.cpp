@@ -1419,7 +1419,11 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   // input tensor every step (a data loader) does not key a new graph.
   // training forwards re-lay the input-gradient weight images on the branch
   // stream (forked / joined inside the forward); one user of it at a time
-  static const bool fwd_side = !(getenv("HCU_FWD_SIDE") && getenv("HCU_FWD_SIDE")[0] == '0');   // A/B
+  // Off by default (HCU_FWD_SIDE=1 enables): measured on MI355X, the forked
+  // re-layout costs the replayed config-2 forward graph 60-110 us per step
+  // (2.15 vs 2.23 ms) and gains nothing on the direct-launch config-3 forward
+  // (6.83 vs 6.82 ms); on the chain the re-layout is one ~12 us launch.
+  static const bool fwd_side = getenv("HCU_FWD_SIDE") && getenv("HCU_FWD_SIDE")[0] == '1';
   const bool split = fwd_side && training && side_enabled() && !timing_on() &&
                      !(p.flags & HCU_PLAN_FORWARD_ONLY);
   std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
