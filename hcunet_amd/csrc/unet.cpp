@@ -1134,6 +1134,8 @@ int graphs_forced() {
 bool graphs_for(const hcu_unet_plan &p, bool backward) {
   const int f = graphs_forced();
   if (f >= 0) return f == 1;
+  static const int fwd = getenv("HCU_FWD_GRAPH") ? atoi(getenv("HCU_FWD_GRAPH")) : -1;   // A/B: 0 / 1
+  if (!backward && fwd >= 0) return fwd == 1;
   return !backward && p.fwd_flops < 100e9;
 }
 
