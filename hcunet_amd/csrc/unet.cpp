@@ -434,6 +434,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 
 #define HCU_NBUF 32   // gradient slots (at most; Ctx::alloc)
 #define HCU_NBUF_RING 6   // ring size when one slot per allocation does not fit
+#define HCU_FORK_RING 16   // marker events of forks that cannot use the chain record
 
 struct hcu_unet_plan {
   hcu_unet_spec spec;
@@ -508,19 +509,25 @@ struct hcu_unet_plan {
   mutable int side_device = -1;
   mutable hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_slot[HCU_NBUF] = {};
   mutable hipEvent_t ev_chain = nullptr;   // stop event of the chain's kernels (Ctx::arm_chain)
+  mutable hipEvent_t ev_prep = nullptr;    // the backward's input-gradient weight images are laid out
+  mutable hipEvent_t ev_fork_ring[HCU_FORK_RING] = {};   // marker forks (Ctx::fork)
+  mutable unsigned fork_next = 0;
   // data-parallel overlap (hcu_unet_set_grad_events): caller-owned events the
   // backward records when the decoder's / the deep encoder levels' gradients are final
   hipEvent_t grad_ev[2] = {nullptr, nullptr};
   int grad_deep = -1;
   void destroy_side() const {
     if (side) (void)hipStreamDestroy(side);
-    for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_chain})
+    for (hipEvent_t *e : {&ev_fork, &ev_join, &ev_chain, &ev_prep})
       if (*e) (void)hipEventDestroy(*e);
     for (hipEvent_t &e : ev_slot)
       if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t &e : ev_fork_ring)
+      if (e) (void)hipEventDestroy(e);
     side = nullptr;
-    ev_fork = ev_join = ev_chain = nullptr;
+    ev_fork = ev_join = ev_chain = ev_prep = nullptr;
     for (hipEvent_t &e : ev_slot) e = nullptr;
+    for (hipEvent_t &e : ev_fork_ring) e = nullptr;
   }
   ~hcu_unet_plan() {
     for (Graph &g : graphs)
@@ -875,8 +882,11 @@ struct Ctx {
       HCU_HIP(hipStreamWaitEvent(ws, p.ev_chain, 0));
       return HCU_OK;
     }
-    HCU_HIP(hipEventRecord(p.ev_fork, s));
-    HCU_HIP(hipStreamWaitEvent(ws, p.ev_fork, 0));
+    // a ring of marker events: re-recording an event whose previous record the
+    // GPU has not reached yet stalls the host (config 3: ~0.9 ms per step)
+    hipEvent_t ev = p.ev_fork_ring[p.fork_next++ % HCU_FORK_RING];
+    HCU_HIP(hipEventRecord(ev, s));
+    HCU_HIP(hipStreamWaitEvent(ws, ev, 0));
     return HCU_OK;
   }
   // Arms the chain record (backward): kernels launched on s from here on
@@ -909,14 +919,23 @@ struct Ctx {
   }
   int join() {
     if (!split) return HCU_OK;
-    HCU_HIP(hipEventRecord(p.ev_join, ws));
-    HCU_HIP(hipStreamWaitEvent(s, p.ev_join, 0));
+    hipEvent_t ev = p.ev_fork_ring[p.fork_next++ % HCU_FORK_RING];
+    HCU_HIP(hipEventRecord(ev, ws));
+    HCU_HIP(hipStreamWaitEvent(s, ev, 0));
     return HCU_OK;
   }
 };
 
 void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
+}
+
+// Off by default (HCU_FWD_SIDE=1 enables): measured on MI355X, the forked
+// re-layout cost the replayed config-2 forward graph 60-110 us per step (2.15
+// vs 2.23 ms) and gained nothing on the direct-launch config-3 forward.
+bool fwd_side_enabled() {
+  static const bool on = getenv("HCU_FWD_SIDE") && getenv("HCU_FWD_SIDE")[0] == '1';
+  return on;
 }
 
 bool bnfin_enabled() {
@@ -1322,7 +1341,10 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
                              t->x_dtype))
       return e;
   tag(std::string("prep"), "fwd");
-  if (training && !p.prep_bwd.empty()) {   // eval forwards never need the dgrad images
+  // training forwards lay out the input-gradient weight images too (on the
+  // chain, or forked with HCU_FWD_SIDE=1); laying them out on the backward's
+  // branch instead measured equal on config 3 and ~10 us slower on config 2
+  if (training && !p.prep_bwd.empty()) {
     if (int e = c.fork()) return e;
     if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
                                 (int)p.prep_bwd.size(), c.wstream()))
@@ -1421,12 +1443,7 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   // input tensor every step (a data loader) does not key a new graph.
   // training forwards re-lay the input-gradient weight images on the branch
   // stream (forked / joined inside the forward); one user of it at a time
-  // Off by default (HCU_FWD_SIDE=1 enables): measured on MI355X, the forked
-  // re-layout costs the replayed config-2 forward graph 60-110 us per step
-  // (2.15 vs 2.23 ms) and gains nothing on the direct-launch config-3 forward
-  // (6.83 vs 6.82 ms); on the chain the re-layout is one ~12 us launch.
-  static const bool fwd_side = getenv("HCU_FWD_SIDE") && getenv("HCU_FWD_SIDE")[0] == '1';
-  const bool split = fwd_side && training && side_enabled() && !timing_on() &&
+  const bool split = fwd_side_enabled() && training && side_enabled() && !timing_on() &&
                      !(p.flags & HCU_PLAN_FORWARD_ONLY);
   std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
   if (split) {
@@ -1637,9 +1654,10 @@ int ensure_side(const hcu_unet_plan &p, int dev) {
   p.destroy_side();
   HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
   p.side_device = dev;
-  for (hipEvent_t *e : {&p.ev_fork, &p.ev_join, &p.ev_chain})
+  for (hipEvent_t *e : {&p.ev_fork, &p.ev_join, &p.ev_chain, &p.ev_prep})
     HCU_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (hipEvent_t &e : p.ev_slot) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipEvent_t &e : p.ev_fork_ring) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return HCU_OK;
 }
 
