@@ -678,10 +678,13 @@ int launch_wgrad(const WGradArgs &a, hipStream_t s) {
 // both the elements and the slabs: S threads share one element (each sums the
 // slabs k = s, s+S, ... in fp64), then the S sums are combined in LDS in a
 // fixed order.  The result is scattered into the PyTorch weight layout.
+// S == 0 selects the tiled form (wgrad_finalize_tile) for the large layers.
 __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int S, double *red);
+__device__ __forceinline__ void wgrad_finalize_tile(const WGradFinalize &f, int bx, float (*tl)[33]);
 __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize f, int S) {
-  __shared__ double red[256];
-  wgrad_finalize_body(f, S, red);
+  __shared__ double sh[528];   // red[256] (S > 0) or the 32 x 33 float tile (S == 0)
+  if (S == 0) wgrad_finalize_tile(f, blockIdx.x, reinterpret_cast<float (*)[33]>(sh));
+  else wgrad_finalize_body(f, S, sh);
 }
 // Several layers' finalizes in one launch (grid.y = job): the backward defers
 // each layer's finalize until its slabs would no longer fit the slab arena.
@@ -692,10 +695,11 @@ struct WGFBatch {
 };
 static_assert(sizeof(WGFBatch) <= 4000, "finalize batch must fit the 4 KB kernel-argument limit");
 __global__ void __launch_bounds__(256) wgrad_finalize_batch_kernel(const WGFBatch b) {
-  __shared__ double red[256];
+  __shared__ double sh[528];
   const int j = blockIdx.y;
   if ((int)blockIdx.x >= b.blocks[j]) return;
-  wgrad_finalize_body(b.f[j], b.S[j], red);
+  if (b.S[j] == 0) wgrad_finalize_tile(b.f[j], blockIdx.x, reinterpret_cast<float (*)[33]>(sh));
+  else wgrad_finalize_body(b.f[j], b.S[j], sh);
 }
 __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int S, double *red) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
@@ -745,12 +749,96 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
   }
 }
 
+// Tiled finalize of the Conv3d (mode 0) / ConvTranspose3d (mode 1) weights:
+// a block sums the slabs of a 32 (column: o / co) x 32 (inner: c*T + t / t)
+// tile of dW, reading along the GEMM column (contiguous in a slab row) and
+// writing along the inner index (contiguous in PyTorch's [Cout][Cin_g][T] /
+// [Cin][Cout][T] layout) through an LDS transpose -- the S == 1 path instead
+// stores one 4-byte word per element with a Cin_g*T (mode 0) or T (mode 1)
+// word stride.  Every destination gathers its own GEMM element (mode 0:
+// e = (g*Cin_g + c) % fold_mod), summed over the slabs k = 0..KB-1 in fp64 in
+// the same order as the S == 1 path, so the results are bitwise equal.
+// Blocks past the tiles finalize the Conv3d bias row.
+__device__ __forceinline__ void wgrad_finalize_tile(const WGradFinalize &f, int bx, float (*tl)[33]) {
+  const int tid = threadIdx.x;
+  const int NC = f.mode == 0 ? f.Cout : f.CoutT;
+  const int NI = f.mode == 0 ? f.Cin_g * f.T : f.T;
+  const int tc = (NC + 31) / 32, ti = (NI + 31) / 32;
+  const int rows = f.mode == 0 ? 1 : f.Cin;
+  const int64_t n = (int64_t)f.Mtot * f.Ntot;
+  if (bx >= rows * tc * ti) {   // mode 0 bias row (grow = T * ACs)
+    const int o = (bx - rows * tc * ti) * 256 + tid;
+    if (o >= f.Cout || !f.db) return;
+    const float *src = f.partial + (int64_t)f.T * f.ACs * f.Ntot + o;
+    double acc = 0.0;
+#pragma unroll 4
+    for (int k = 0; k < f.KB; ++k) acc += (double)src[(size_t)k * n];
+    const float v = (float)acc;
+    f.db[o] = f.accumulate ? f.db[o] + v : v;
+    return;
+  }
+  const int row = bx / (tc * ti), rem = bx % (tc * ti);
+  const int c0 = (rem % tc) * 32, i0 = (rem / tc) * 32;
+  const int cl = tid & 31, col = c0 + cl;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int il = (tid >> 5) + 8 * r, in = i0 + il;
+    double acc = 0.0;
+    if (col < NC && in < NI) {
+      int64_t idx;
+      if (f.mode == 0) {
+        const int c = in / f.T, t = in % f.T;
+        const int e = (col / (f.Cout / f.groups) * f.Cin_g + c) % f.fold_mod;
+        idx = (int64_t)(t * f.ACs + e) * f.Ntot + col;
+      } else {
+        idx = (int64_t)row * f.Ntot + (int64_t)in * f.GCs + col;
+      }
+      const float *src = f.partial + idx;
+#pragma unroll 4
+      for (int k = 0; k < f.KB; ++k) acc += (double)src[(size_t)k * n];
+    }
+    tl[il][cl] = (float)acc;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int p = tid + 256 * r, il = p & 31, cl2 = p >> 5;
+    const int in = i0 + il, col2 = c0 + cl2;
+    if (col2 >= NC || in >= NI) continue;
+    float *dst = f.mode == 0 ? f.dw + (size_t)col2 * NI + in
+                             : f.dw + ((size_t)row * f.CoutT + col2) * f.T + in;
+    const float v = tl[il][cl2];
+    *dst = f.accumulate ? *dst + v : v;
+  }
+}
+
+// HCU_WGF_TILED: 0 keeps every finalize on the element-parallel form, 1 (the
+// default) tiles the layers that need no slab parallelism, 2 tiles every
+// Conv3d / ConvTranspose3d finalize (A/B and tests)
+static int tiled_finalize_mode() {
+  static const int m = [] {
+    const char *e = getenv("HCU_WGF_TILED");
+    return e && e[0] ? atoi(e) : 1;
+  }();
+  return m;
+}
+
 static void wgf_geometry(const WGradFinalize &f, int &S, int &blocks) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
   S = 1;
   while (S < 64 && S * 2 <= f.KB && n * S / 256 < 1024) S *= 2;
   const int EPB = 256 / S;
   blocks = (int)((n + EPB - 1) / EPB);
+  // large layers (no slab parallelism needed): the coalescing tiled form
+  const int tm = tiled_finalize_mode();
+  if ((tm == 2 || (tm == 1 && S == 1)) && (f.mode == 1 || (f.mode == 0 && f.fold_mod > 0))) {
+    const int NC = f.mode == 0 ? f.Cout : f.CoutT;
+    const int NI = f.mode == 0 ? f.Cin_g * f.T : f.T;
+    const int rows = f.mode == 0 ? 1 : f.Cin;
+    S = 0;
+    blocks = rows * ((NC + 31) / 32) * ((NI + 31) / 32);
+    if (f.mode == 0 && f.Mtot > f.T * f.ACs) blocks += (f.Cout + 255) / 256;
+  }
 }
 
 int launch_wgrad_finalize_batch(const WGradFinalize *fs, int n, hipStream_t s) {

@@ -114,3 +114,21 @@ def test_fresh_input_every_step_matches():
     for a_it, b_it in zip(*res):
         for a, b in zip(a_it, b_it):
             assert torch.equal(a, b)
+
+
+def test_tiled_weight_gradient_finalize(tmp_path):
+    """HCU_WGF_TILED=2 (every Conv3d / ConvTranspose3d weight-gradient finalize
+    through the coalescing LDS-transposed tile) agrees with HCU_WGF_TILED=0
+    (element-parallel slab sums, scattered stores) to fp64-summation rounding:
+    both sum the same fp32 slabs in fp64, only the order over the slabs may
+    differ (S > 1 splits them), so every gradient matches to 2 fp32 ulps of its
+    largest element.  Outputs are bitwise equal (step 1) and each mode is
+    deterministic."""
+    off = _run(tmp_path, 'wgf0', {'HCU_WGF_TILED': '0'})
+    on = _run(tmp_path, 'wgf2', {'HCU_WGF_TILED': '2'})
+    on2 = _run(tmp_path, 'wgf2b', {'HCU_WGF_TILED': '2'})
+    assert torch.equal(off[0][0], on[0][0])
+    for a, b, c in zip(off[0], on[0], on2[0]):
+        assert torch.equal(b, c)
+        tol = 2.5e-7 * max(a.abs().max().item(), 1e-30)
+        assert (a - b).abs().max().item() <= tol
