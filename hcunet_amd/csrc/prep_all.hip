@@ -7,6 +7,7 @@
 #include "common.h"
 #include "timing.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace hcu {
 
@@ -101,8 +102,21 @@ __device__ float prep_value(const PrepJob &jb, const float *w, uint32_t i) {
   return prep_decode(jb, i, t, a, b) ? prep_eval(jb, w, t, a, b) : 0.f;
 }
 
+// Packed images are [chunk][s][g][column][V]: consecutive vectors k walk the
+// output column, whose source weights lie Cin_g*T floats apart, so a wave's
+// gather touched 64 lines per element and a large layer's weights were
+// re-fetched once per tap (3.6x the parameter bytes).  The vector a thread
+// handles is taken column-major instead (perm): the lanes of a wave share the
+// column and walk (g, s), i.e. the tap, whose source weights are adjacent.
+// Same values, same image; the 16-byte stores scatter instead.
+__device__ __forceinline__ uint32_t prep_perm(uint32_t u, uint32_t nv, uint32_t cw, bool on) {
+  if (!on) return u;
+  const uint32_t r = nv / cw;
+  return (u % r) * cw + u / r;
+}
+
 __global__ void __launch_bounds__(256)
-prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
+prep_all_kernel(const float *params, float *dst_base, const PrepBatch b, int perm) {
   const PrepJob &jb = b.j[blockIdx.y];
   const float *w = params + jb.src;
   float *dst = dst_base + jb.dst;
@@ -110,9 +124,12 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
   // packed images: one decode per 16-byte vector (8 bf16 / 4 fp32 elements
   // whose middle index advances by one), one 16-byte store
   if (jb.pk.on && jb.kind != PREP_CONVT_PHASE && ((uintptr_t)dst & 15) == 0) {
+    const uint32_t cw = (uint32_t)(jb.pk.CoutW > 0 ? jb.pk.CoutW : 1);
     if (jb.bf16 && jb.pk.on == 3 && n % 8 == 0) {
       uint4 *d = reinterpret_cast<uint4 *>(dst);
-      for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n / 8; k += gridDim.x * 256) {
+      const bool pm = perm && (n / 8) % cw == 0;
+      for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < n / 8; u += gridDim.x * 256) {
+        const uint32_t k = prep_perm(u, n / 8, cw, pm);
         int t, a, b;
         const bool ok = prep_decode(jb, k * 8, t, a, b);
         float v[8];
@@ -127,7 +144,9 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
     }
     if (!jb.bf16 && jb.pk.on != 3 && n % 4 == 0) {
       float4 *d = reinterpret_cast<float4 *>(dst);
-      for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n / 4; k += gridDim.x * 256) {
+      const bool pm = perm && jb.pk.on == 1 && (n / 4) % cw == 0;
+      for (uint32_t u = blockIdx.x * 256 + threadIdx.x; u < n / 4; u += gridDim.x * 256) {
+        const uint32_t k = prep_perm(u, n / 4, cw, pm);
         int t, a, b;
         const bool ok = prep_decode(jb, k * 4, t, a, b);
         float v[4];
@@ -150,6 +169,11 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b) {
 
 int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n,
                     hipStream_t s) {
+  // HCU_PREP_PERM=0: the column-fastest vector order (A/B)
+  static const int perm = [] {
+    const char *e = getenv("HCU_PREP_PERM");
+    return !(e && e[0] == '0');
+  }();
   for (int j0 = 0; j0 < n; j0 += kPrepBatch) {
     PrepBatch b{};
     b.n = std::min(kPrepBatch, n - j0);
@@ -163,7 +187,7 @@ int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, i
     const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((most + 2047) / 2048, 1024));
     HCU_TIMED(s, "prep_all_kernel", 0.0, 0.0,
               HCU_LAUNCH(prep_all_kernel, dim3(gx, b.n), dim3(256), 0, s, params,
-                                 dst_base, b));
+                                 dst_base, b, perm));
     HCU_CHECK_LAUNCH();
   }
   return 0;
