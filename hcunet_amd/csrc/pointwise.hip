@@ -116,8 +116,25 @@ bn_fwd_finalize_kernel(const float *stats, int R, int W, int C, double count,
   const int c = blockIdx.x, tid = threadIdx.x;
   double m = 0.0, v = 0.0;
   if (training && c < C) {
+    // a thread's first RC rows are loaded together (independent loads in
+    // flight) and kept in registers for the second pass; the summation order
+    // is the plain r = tid, tid + 256, ... order either way
+    constexpr int RC = 8;
+    float4 rows[RC];
+#pragma unroll
+    for (int k = 0; k < RC; ++k) {
+      const int r = tid + 256 * k;
+      rows[k] = r < R ? *reinterpret_cast<const float4 *>(stats + ((size_t)r * W + c) * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     double t = 0.0, nn = 0.0;
-    for (int r = tid; r < R; r += 256) {
+#pragma unroll
+    for (int k = 0; k < RC; ++k)
+      if (rows[k].w > 0.f) {
+        t += (double)rows[k].x + (double)rows[k].w * (double)rows[k].z;
+        nn += (double)rows[k].w;
+      }
+    for (int r = tid + 256 * RC; r < R; r += 256) {
       const float4 row = *reinterpret_cast<const float4 *>(stats + ((size_t)r * W + c) * 4);
       if (row.w > 0.f) {
         t += (double)row.x + (double)row.w * (double)row.z;
@@ -128,7 +145,14 @@ bn_fwd_finalize_kernel(const float *stats, int R, int W, int C, double count,
     const double ntot = block_sum_f64(nn, red);
     m = tot / ntot;
     double q = 0.0;
-    for (int r = tid; r < R; r += 256) {
+#pragma unroll
+    for (int k = 0; k < RC; ++k)
+      if (rows[k].w > 0.f) {
+        const double n = rows[k].w, s1 = rows[k].x;
+        const double d = (double)rows[k].z + s1 / n - m;
+        q += ((double)rows[k].y - s1 * s1 / n) + n * d * d;
+      }
+    for (int r = tid + 256 * RC; r < R; r += 256) {
       const float4 row = *reinterpret_cast<const float4 *>(stats + ((size_t)r * W + c) * 4);
       if (row.w > 0.f) {
         const double n = row.w, s1 = row.x;
@@ -189,9 +213,11 @@ bn_bwd_finalize_kernel(const float *part, int R, int C, int W, double count,
   const int c = blockIdx.x, tid = threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
+#pragma unroll 8
     for (int r = tid; r < R; r += 256) {
-      s1 += (double)part[((size_t)r * W + c) * 2 + 0];
-      s2 += (double)part[((size_t)r * W + c) * 2 + 1];
+      const float2 p2 = *reinterpret_cast<const float2 *>(part + ((size_t)r * W + c) * 2);
+      s1 += (double)p2.x;
+      s2 += (double)p2.y;
     }
   }
 #pragma unroll
