@@ -201,12 +201,15 @@ def layer_table(detail, cfg, B, steps):
     return out
 
 
-def rocprof_avg_us(kernel, config):
+def rocprof_avg_us(kernel, config, kind=''):
     """Average duration (us) of `kernel` in the committed rocprofv3
-    --kernel-trace --stats summary of this config's graphed bench step
-    (profiles/<PROFILE_TAG>_kernel_stats_config<config>.csv), or None."""
+    --kernel-trace --stats summary of this config's bench step
+    (profiles/<PROFILE_TAG>_kernel_stats_<kind>config<config>.csv), or None.
+    kind '' is the production step (weight-gradient branch concurrent with the
+    chain); 'serial_' the same bench with HCU_SIDE=0, one kernel at a time --
+    the conditions of the HIP-event timing pass."""
     import csv
-    path = os.path.join(ROOT, 'profiles', '%s_kernel_stats_config%s.csv' % (PROFILE_TAG, config))
+    path = os.path.join(ROOT, 'profiles', '%s_kernel_stats_%sconfig%s.csv' % (PROFILE_TAG, kind, config))
     try:
         with open(path, newline='') as f:
             rows = list(csv.DictReader(f))
@@ -513,14 +516,22 @@ def main():
             ach = d['bytes'] / d['count'] / avg_s / 1e9
             bound, peak, unit = 'hbm', PEAK_HBM_GBS, 'GB/s'
         rp_us = rocprof_avg_us(name, args.config)
+        rp_serial_us = rocprof_avg_us(name, args.config, 'serial_')
         per_launch = (d['flops'] if d['flops'] > 0 else d['bytes']) / d['count']
+        scale = 1e12 if d['flops'] > 0 else 1e9
         roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit,
                     "frac": ach / peak, "traffic": load_traffic(name, args.config), "kernel": name,
+                    # HIP events around each launch, kernels serialized (timing pass)
                     "avg_launch_us": avg_s * 1e6,
+                    # rocprofv3 --stats of the serialized step (HCU_SIDE=0): the
+                    # same conditions, so it must agree with avg_launch_us
+                    "rocprof_serial_avg_launch_us": rp_serial_us,
+                    # rocprofv3 --stats of the production step: the weight-gradient
+                    # branch shares the CUs with the chain, so its kernels run longer
                     "rocprof_avg_launch_us": rp_us,
-                    # the same fraction from the committed rocprofv3 summary's average
-                    "frac_rocprof": (per_launch / (rp_us * 1e-6) / (1e12 if d['flops'] > 0 else 1e9) / peak
-                                     if rp_us else None),
+                    "frac_rocprof_serial": (per_launch / (rp_serial_us * 1e-6) / scale / peak
+                                            if rp_serial_us else None),
+                    "frac_rocprof": (per_launch / (rp_us * 1e-6) / scale / peak if rp_us else None),
                     "launches_per_step": d['count'] / args.steps,
                     "flops_per_launch": d['flops'] / d['count'],
                     "share_of_kernel_time": d['ms'] / total_ms}

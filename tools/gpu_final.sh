@@ -22,6 +22,12 @@ for C in 2 3; do
     > $O/${TAG}_prof$C.log 2>&1 || { tail -30 $O/${TAG}_prof$C.log; exit 1; }
   f=$(find $O/${TAG}_prof$C -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_config$C.csv
   echo "rocprof config $C: $(head -3 $O/${TAG}_kernel_stats_config$C.csv | tail -2 | cut -c1-120)"
+  # the same bench with the backward on one stream: kernel durations under the
+  # conditions of bench.py's serialized HIP-event timing pass
+  HCU_SIDE=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_profs$C \
+    -- python3 bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing \
+    > $O/${TAG}_profs$C.log 2>&1 || { tail -30 $O/${TAG}_profs$C.log; exit 1; }
+  f=$(find $O/${TAG}_profs$C -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_serial_config$C.csv
   timeout -k 10 300 rocprofv3 --kernel-trace -d $O/${TAG}_tl$C \
     -- python3 bench.py --config $C --steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing \
     > $O/${TAG}_tl$C.log 2>&1 || { tail -30 $O/${TAG}_tl$C.log; exit 1; }
@@ -41,8 +47,16 @@ for C in 2 3; do
   bash tools/pmc_sq.sh ${TAG}_sq$C $C > $O/${TAG}_sq$C.log 2>&1 || { tail -20 $O/${TAG}_sq$C.log; exit 1; }
   cp $O/${TAG}_sq${C}_summary.txt $O/${TAG}_sq_counters_config$C.txt
   echo "sq counters config $C done"
-  find $O/${TAG}_fetch$C $O/${TAG}_write$C $O/${TAG}_prof$C $O/${TAG}_tl$C -name '*.csv' -size +20M -delete 2>/dev/null
+  find $O/${TAG}_fetch$C $O/${TAG}_write$C $O/${TAG}_prof$C $O/${TAG}_profs$C $O/${TAG}_tl$C -name '*.csv' -size +20M -delete 2>/dev/null
   find $O/${TAG}_tl$C -name '*.db' -delete 2>/dev/null
+done
+# the bench lines cite profiles/r03_* (bench.py PROFILE_TAG): install this
+# pass's summaries there first (in the box's copy; the results come back via
+# gpurun_out/ and are committed from there)
+for C in 2 3; do
+  cp $O/${TAG}_kernel_stats_config$C.csv profiles/r03_kernel_stats_config$C.csv
+  cp $O/${TAG}_kernel_stats_serial_config$C.csv profiles/r03_kernel_stats_serial_config$C.csv
+  [ -s $O/${TAG}_traffic_config$C.json ] && cp $O/${TAG}_traffic_config$C.json profiles/r03_traffic_config$C.json
 done
 for C in 2 3; do
   timeout -k 10 300 python -u bench.py --config $C --steps 20 --warmup 3 > $O/${TAG}_bench_config$C.json 2> $O/${TAG}_bench_config$C.err \
