@@ -1652,7 +1652,17 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
 int ensure_side(const hcu_unet_plan &p, int dev) {
   if (p.side && p.side_device == dev) return HCU_OK;
   p.destroy_side();
-  HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+  // HCU_SIDE_PRIO=1 / -1: the weight-gradient branch at the device's greatest /
+  // least stream priority (A/B; default: the normal priority of the chain)
+  const char *pe = getenv("HCU_SIDE_PRIO");
+  const int pv = pe ? atoi(pe) : 0;
+  if (pv != 0) {
+    int least = 0, greatest = 0;
+    HCU_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HCU_HIP(hipStreamCreateWithPriority(&p.side, hipStreamNonBlocking, pv > 0 ? greatest : least));
+  } else {
+    HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+  }
   p.side_device = dev;
   for (hipEvent_t *e : {&p.ev_fork, &p.ev_join, &p.ev_chain, &p.ev_prep})
     HCU_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
