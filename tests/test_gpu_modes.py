@@ -24,18 +24,16 @@ sys.path.insert(0, %(root)r)
 from hcat.unet import Unet_Constructor
 from hcat.loss import cross_entropy
 from oracle import inputs
-kw = dict(image_dimensions=3, in_channels=4, out_channels=1, feature_sizes=[8, 16, 32, 64, 128],
-          kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)}, upsample_kernel=(2, 2, 2),
-          max_pool_kernel=(2, 2, 1), upsample_stride=(2, 2, 1))
+kw = %(kw)s
 torch.manual_seed(0)
 m = Unet_Constructor(**kw).cuda().train()
-x = torch.from_numpy(inputs.make_x((2, 4, 188, 188, 6))).cuda()
+x = torch.from_numpy(inputs.make_x(%(shape)r)).cuda()
 res = []
 for it in range(3):          # 3 steps: the graphed mode replays its capture
     for p in m.parameters():
         p.grad = None
     out = m(x)
-    ms = (2, 1) + tuple(out.shape[2:])
+    ms = (x.shape[0], 1) + tuple(out.shape[2:])
     loss = cross_entropy(out, torch.from_numpy(inputs.make_mask(ms)).cuda(),
                          torch.from_numpy(inputs.make_pwl(ms)).cuda(), method='pixel')
     loss.backward()
@@ -45,12 +43,24 @@ torch.save(res, %(out)r)
 '''
 
 
-def _run(tmp_path, tag, env_extra):
+KW = ("dict(image_dimensions=3, in_channels=4, out_channels=1, feature_sizes=[8, 16, 32, 64, 128], "
+      "kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)}, upsample_kernel=(2, 2, 2), "
+      "max_pool_kernel=(2, 2, 1), upsample_stride=(2, 2, 1))")
+SHAPE = (2, 4, 188, 188, 6)
+# the inference network of hcat/main.py:46-54: grouped convolutions (groups=2)
+# and an (8, 8, 2) ConvTranspose3d kernel
+KW_GROUPS = ("dict(image_dimensions=3, in_channels=4, out_channels=1, feature_sizes=[16, 32, 64], "
+             "kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)}, upsample_kernel=(8, 8, 2), "
+             "max_pool_kernel=(2, 2, 1), upsample_stride=(2, 2, 1), dilation=1, groups=2)")
+SHAPE_GROUPS = (1, 4, 64, 60, 6)   # test_gpu_unet.py's g2_up8 geometry
+
+
+def _run(tmp_path, tag, env_extra, kw=KW, shape=SHAPE):
     out = str(tmp_path / ('%s.pt' % tag))
     env = dict(os.environ)
     env.update(env_extra)
     env['HCU_BCONV_TUNE'] = '0'   # measured tile choices may differ between processes
-    r = subprocess.run([sys.executable, '-c', CHILD % dict(root=ROOT, out=out)], env=env,
+    r = subprocess.run([sys.executable, '-c', CHILD % dict(root=ROOT, out=out, kw=kw, shape=shape)], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     return torch.load(out, weights_only=True)
@@ -127,8 +137,12 @@ def test_tiled_weight_gradient_finalize(tmp_path):
     off = _run(tmp_path, 'wgf0', {'HCU_WGF_TILED': '0'})
     on = _run(tmp_path, 'wgf2', {'HCU_WGF_TILED': '2'})
     on2 = _run(tmp_path, 'wgf2b', {'HCU_WGF_TILED': '2'})
-    assert torch.equal(off[0][0], on[0][0])
-    for a, b, c in zip(off[0], on[0], on2[0]):
-        assert torch.equal(b, c)
-        tol = 2.5e-7 * max(a.abs().max().item(), 1e-30)
-        assert (a - b).abs().max().item() <= tol
+    # grouped convolutions and a ConvTranspose3d with 128 taps
+    goff = _run(tmp_path, 'gwgf0', {'HCU_WGF_TILED': '0'}, KW_GROUPS, SHAPE_GROUPS)
+    gon = _run(tmp_path, 'gwgf2', {'HCU_WGF_TILED': '2'}, KW_GROUPS, SHAPE_GROUPS)
+    for r0, r2, r2b in ((off, on, on2), (goff, gon, gon)):
+        assert torch.equal(r0[0][0], r2[0][0])
+        for a, b, c in zip(r0[0], r2[0], r2b[0]):
+            assert torch.equal(b, c)
+            tol = 2.5e-7 * max(a.abs().max().item(), 1e-30)
+            assert (a - b).abs().max().item() <= tol
