@@ -1324,6 +1324,7 @@ int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int 
 
 int ensure_side(const hcu_unet_plan &p, int dev);
 bool side_enabled();
+bool wgf_early();
 
 static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,
                            hipStream_t stream, bool input_done = false, bool split = false) {
@@ -1622,6 +1623,10 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.alloc(sa)) return e;
       dIn = c.buf(sa);
     }
+    // the last weight gradient waits for the chain's last BatchNorm backward:
+    // the pending finalizes run on the branch in that window instead of after it
+    if (i == 0 && wgf_early())
+      if (int e = c.flush_wgf()) return e;
     if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training,
                               nullptr, false, gap && done1 ? &c1 : nullptr))
       return e;
@@ -1669,6 +1674,11 @@ int ensure_side(const hcu_unet_plan &p, int dev) {
   for (hipEvent_t &e : p.ev_slot) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (hipEvent_t &e : p.ev_fork_ring) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return HCU_OK;
+}
+
+bool wgf_early() {   // HCU_WGF_EARLY=1: flush the pending finalizes before the first layer's wgrad
+  static const bool on = getenv("HCU_WGF_EARLY") && getenv("HCU_WGF_EARLY")[0] == '1';
+  return on;
 }
 
 bool side_enabled() {   // HCU_SIDE=0 keeps the whole backward on one stream (A/B, debugging)
