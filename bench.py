@@ -61,8 +61,9 @@ CONFIGS = {
                       upsample_stride=(2, 2, 1)),
               batch=4, dtype='bf16', roof_ms=0.891,
               desc='config 3: 3D U-Net feature_sizes=[32,64,128,256,512] bf16 (autocast)'),
-    # BASELINE config 3's shapes ([32..512], B=4) computed in fp32: the bf16
-    # path is not built, so this is a capacity/shape check, not config 3 itself.
+    # BASELINE config 3's shapes ([32..512], B=4) computed in fp32: a
+    # capacity/shape check of the fp32 path at those sizes, not config 3
+    # itself (config 3 is the bf16 line above).
     '3f32': dict(kw=dict(image_dimensions=3, in_channels=4, out_channels=1,
                          feature_sizes=[32, 64, 128, 256, 512],
                          kernel={'conv1': (3, 3, 2), 'conv2': (3, 3, 1)},

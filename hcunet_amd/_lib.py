@@ -132,6 +132,7 @@ SYMBOLS = [
     ("hcu_gate_bwd", _I, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_gather_vectors", _I, [ctypes.POINTER(_VP), ctypes.POINTER(_I), _I, _VP, _I, _VP]),
     ("hcu_unet_set_grad_events", _I, [_VP, _VP, _VP, _I]),
+    ("hcu_unet_grad_events_live", _I, [_VP]),
     ("hcu_event_create", _I, [ctypes.POINTER(_VP)]),
     ("hcu_event_destroy", _I, [_VP]),
     ("hcu_stream_wait_event", _I, [_VP, _VP]),

@@ -781,8 +781,7 @@ int build_plan(hcu_unet_plan &p) {
     // a U-Net backward allocates 1 + 3 slots per decoder level + at most 3 per
     // encoder level: one slot each when that stays within 32 slots and 24 GB
     const int need = 1 + 3 * (L - 1) + 3 * L;
-    p.no_reuse = !fwd_only && need <= HCU_NBUF && (double)need * p.max_act * 4.0 <= 24e9 &&
-                 !(getenv("HCU_GRAD_RING") && getenv("HCU_GRAD_RING")[0] == '1');   // A/B
+    p.no_reuse = !fwd_only && need <= HCU_NBUF && (double)need * p.max_act * 4.0 <= 24e9;
     p.nbuf = p.no_reuse ? need : HCU_NBUF_RING;
     for (int i = 0; i < HCU_NBUF; ++i)
       p.buf_off[i] = scratch.take_floats(fwd_only || i >= p.nbuf ? 0 : p.max_act);
@@ -873,9 +872,6 @@ struct Ctx {
   // Branch work issued from here on sees everything the main chain has issued.
   int fork() {
     if (!split) return HCU_OK;
-    // HCU_FORK_DUP=N (measurement): N extra markers on the chain per fork
-    static const int dup = getenv("HCU_FORK_DUP") ? atoi(getenv("HCU_FORK_DUP")) : 0;
-    for (int k = 0; k < dup; ++k) HCU_HIP(hipEventRecord(p.ev_fork, s));
     const ChainRec &r = chain_rec();
     if (r.ev == p.ev_chain && r.s == s && r.n > chain_n0) {
       // the chain's last kernel carries ev_chain as its stop event (HCU_LAUNCH)
@@ -894,8 +890,7 @@ struct Ctx {
   unsigned long chain_n0 = 0;
   bool armed = false;
   void arm_chain() {
-    static const bool off = getenv("HCU_FORK_MARKERS") && getenv("HCU_FORK_MARKERS")[0] == '1';   // A/B
-    if (!split || off || !p.ev_chain) return;
+    if (!split || !p.ev_chain) return;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // captured graphs keep their markers
     if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
       (void)hipGetLastError();
@@ -928,14 +923,6 @@ struct Ctx {
 
 void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
-}
-
-// Off by default (HCU_FWD_SIDE=1 enables): measured on MI355X, the forked
-// re-layout cost the replayed config-2 forward graph 60-110 us per step (2.15
-// vs 2.23 ms) and gained nothing on the direct-launch config-3 forward.
-bool fwd_side_enabled() {
-  static const bool on = getenv("HCU_FWD_SIDE") && getenv("HCU_FWD_SIDE")[0] == '1';
-  return on;
 }
 
 bool bnfin_enabled() {
@@ -1153,8 +1140,6 @@ int graphs_forced() {
 bool graphs_for(const hcu_unet_plan &p, bool backward) {
   const int f = graphs_forced();
   if (f >= 0) return f == 1;
-  static const int fwd = getenv("HCU_FWD_GRAPH") ? atoi(getenv("HCU_FWD_GRAPH")) : -1;   // A/B: 0 / 1
-  if (!backward && fwd >= 0) return fwd == 1;
   return !backward && p.fwd_flops < 100e9;
 }
 
@@ -1275,10 +1260,19 @@ int hcu_unet_set_grad_events(hcu_unet_plan *p, void *ev_decoder, void *ev_deep, 
   if (!p || p->is_chain) return fail(HCU_ERR_INVALID, "hcu_unet_set_grad_events: U-Net plan required");
   if (ev_deep && (deep_level < 1 || deep_level >= p->L))
     return fail(HCU_ERR_INVALID, "hcu_unet_set_grad_events: deep_level must be in [1, levels)");
+  std::lock_guard<std::mutex> lk(p->smu);   // enqueue_backward reads them under the same lock
   p->grad_ev[0] = (hipEvent_t)ev_decoder;
   p->grad_ev[1] = (hipEvent_t)ev_deep;
   p->grad_deep = ev_deep ? deep_level : -1;
   return HCU_OK;
+}
+
+// 1 when hcu_unet_backward records the events set by hcu_unet_set_grad_events
+// (a direct-launch backward), 0 when it does not (a backward replayed from a
+// captured graph: the caller must then reduce after the whole backward).
+int hcu_unet_grad_events_live(const hcu_unet_plan *p) {
+  if (!p || p->is_chain) return 0;
+  return (graphs_for(*p, true) && !timing_on()) ? 0 : 1;
 }
 
 int hcu_event_create(void **ev) {
@@ -1324,7 +1318,6 @@ int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int 
 
 int ensure_side(const hcu_unet_plan &p, int dev);
 bool side_enabled();
-bool wgf_early();
 
 static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,
                            hipStream_t stream, bool input_done = false, bool split = false) {
@@ -1342,9 +1335,9 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
                              t->x_dtype))
       return e;
   tag(std::string("prep"), "fwd");
-  // training forwards lay out the input-gradient weight images too (on the
-  // chain, or forked with HCU_FWD_SIDE=1); laying them out on the backward's
-  // branch instead measured equal on config 3 and ~10 us slower on config 2
+  // training forwards lay out the input-gradient weight images too; laying
+  // them out on the backward's branch instead measured equal on config 3 and
+  // ~10 us slower on config 2
   if (training && !p.prep_bwd.empty()) {
     if (int e = c.fork()) return e;
     if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
@@ -1442,17 +1435,10 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   }
   // The input layout change runs ahead of the captured sequence, so a fresh
   // input tensor every step (a data loader) does not key a new graph.
-  // training forwards re-lay the input-gradient weight images on the branch
-  // stream (forked / joined inside the forward); one user of it at a time
-  const bool split = fwd_side_enabled() && training && side_enabled() && !timing_on() &&
-                     !(p.flags & HCU_PLAN_FORWARD_ONLY);
-  std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
-  if (split) {
-    lk.lock();
-    int dev = 0;
-    HCU_HIP(hipGetDevice(&dev));
-    if (int e = ensure_side(p, dev)) return e;
-  }
+  // (the forward runs on the caller's stream alone: forking the input-gradient
+  // weight re-layout onto the branch measured 60-110 us slower per config-2
+  // step in round 3)
+  const bool split = false;
   if (graphs_for(p, false) && !timing_on()) {
     tag(std::string("in"), "fwd");
     if (int e = launch_to_cl(t->x, reinterpret_cast<float *>((char *)t->saved + p.xcl_off), p.B, p.xin.C,
@@ -1469,7 +1455,7 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
 
 static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout,
                             float *dx, int training, int accumulate, hipStream_t stream,
-                            bool split) {
+                            bool split, bool record_grad_events) {
   const hcu_unet_spec &s = p.spec;
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   c.split = split;
@@ -1593,8 +1579,10 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
   // Data-parallel overlap: every gradient of a finished group is written by
   // the finalizes pending on the branch and by kernels the main chain issued
   // before this point; the branch flushes, joins the chain (fork) and records.
+  // (not in a captured backward: a record inside stream capture is only a
+  // capture dependency, a replay would never record the caller's events)
   auto grads_ready = [&](hipEvent_t ev) -> int {
-    if (!ev) return 0;
+    if (!ev || !record_grad_events) return 0;
     if (int e = c.flush_wgf()) return e;
     if (int e = c.fork()) return e;
     HCU_HIP(hipEventRecord(ev, c.wstream()));
@@ -1623,10 +1611,6 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.alloc(sa)) return e;
       dIn = c.buf(sa);
     }
-    // the last weight gradient waits for the chain's last BatchNorm backward:
-    // the pending finalizes run on the branch in that window instead of after it
-    if (i == 0 && wgf_early())
-      if (int e = c.flush_wgf()) return e;
     if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training,
                               nullptr, false, gap && done1 ? &c1 : nullptr))
       return e;
@@ -1657,28 +1641,14 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
 int ensure_side(const hcu_unet_plan &p, int dev) {
   if (p.side && p.side_device == dev) return HCU_OK;
   p.destroy_side();
-  // HCU_SIDE_PRIO=1 / -1: the weight-gradient branch at the device's greatest /
-  // least stream priority (A/B; default: the normal priority of the chain)
-  const char *pe = getenv("HCU_SIDE_PRIO");
-  const int pv = pe ? atoi(pe) : 0;
-  if (pv != 0) {
-    int least = 0, greatest = 0;
-    HCU_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HCU_HIP(hipStreamCreateWithPriority(&p.side, hipStreamNonBlocking, pv > 0 ? greatest : least));
-  } else {
-    HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
-  }
+  // (stream priority of the branch, either way, measured no effect in round 3)
+  HCU_HIP(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
   p.side_device = dev;
   for (hipEvent_t *e : {&p.ev_fork, &p.ev_join, &p.ev_chain, &p.ev_prep})
     HCU_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   for (hipEvent_t &e : p.ev_slot) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   for (hipEvent_t &e : p.ev_fork_ring) HCU_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return HCU_OK;
-}
-
-bool wgf_early() {   // HCU_WGF_EARLY=1: flush the pending finalizes before the first layer's wgrad
-  static const bool on = getenv("HCU_WGF_EARLY") && getenv("HCU_WGF_EARLY")[0] == '1';
-  return on;
 }
 
 bool side_enabled() {   // HCU_SIDE=0 keeps the whole backward on one stream (A/B, debugging)
@@ -1710,8 +1680,9 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
     if (int e = ensure_side(p, dev)) return e;
   }
   key.push_back((uintptr_t)split);
+  const bool live = graphs_for(p, true) && !timing_on() ? false : true;
   return run_graphed(p, key, (hipStream_t)stream, [&](hipStream_t s) {
-    return enqueue_backward(p, t, dout, dx, training, accumulate, s, split);
+    return enqueue_backward(p, t, dout, dx, training, accumulate, s, split, live);
   });
 }
 

@@ -22,13 +22,18 @@ def _avg_supported(group=None):
 
 
 def _running_stats(module, with_stats):
+    """The BatchNorm running mean/var buffers reduced with the gradients: the
+    Unet_Constructor's in the layout its engine reserves room for
+    (bn_modules order), any other module's (RecursiveUnet, RDCNet, user
+    networks: /root/reference/hcat/r_unet.py:276-277,326-327) in
+    module.modules() order -- the same order on every rank."""
     if not with_stats:
         return []
     from .unet import bn_modules
     try:
         bns = bn_modules(module)
-    except AttributeError:   # not a Unet_Constructor: reduce gradients only
-        return []
+    except AttributeError:
+        bns = [m for m in module.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
     return [bn.running_mean for bn in bns if bn.running_mean is not None] + \
            [bn.running_var for bn in bns if bn.running_var is not None]
 
@@ -149,7 +154,12 @@ def allreduce_gradients(module, group=None, bn_stats=True):
             and C.numel() >= G.numel() + nstat
     native = flat_ok and C.is_cuda and 0 < len(stats) <= 128 and all(t.is_contiguous() for t in stats)
     ev = getattr(eng, 'grad_events', None) if eng is not None else None
-    if native and ev is not None and eng.events_recorded:
+    # the overlapped ranges wait only for the backward's own events: any
+    # in-place gradient work queued since (a changed version counter) makes
+    # this step take the single collective behind the caller's stream
+    untouched = eng is not None and getattr(eng, 'grad_version', None) is not None \
+        and G is not None and G._version == eng.grad_version
+    if native and ev is not None and eng.events_recorded and untouched:
         ranges = bucket_ranges(module, ev[2], nstat)
         if ranges is not None and ranges[0][1] == G.numel() + nstat:
             _allreduce_overlapped(eng, C[:G.numel() + nstat], G.numel(), stats, ranges, ev, group, world)

@@ -406,6 +406,7 @@ class _Engine:
         # last backward recorded them into grad_flat
         self.grad_events = None      # (ev_decoder, ev_deep, deep_level) or None
         self.events_recorded = False
+        self.grad_version = None     # grad_flat._version right after the last backward
 
     def check_input(self, x, bf16=False):
         m = self.module_ref
@@ -627,17 +628,25 @@ class _UnetFunction(torch.autograd.Function):
         G, accumulate, finish = eng.grad_target()
         t = eng.tensors(x, None, saved, scratch, grads=G)
         ev = eng.grad_events if G is eng.grad_flat else None
-        _lib.check(_lib.lib().hcu_unet_set_grad_events(
+        L = _lib.lib()
+        if ev is not None and not L.hcu_unet_grad_events_live(plan.handle):
+            ev = None   # a replayed (graphed) backward does not record them
+        _lib.check(L.hcu_unet_set_grad_events(
             plan.handle, ev[0] if ev else None, ev[1] if ev else None, ev[2] if ev else 0),
             'Unet_Constructor.backward')
         eng.events_recorded = ev is not None
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().hcu_unet_backward(plan.handle, ctypes.byref(t),
-                                                    ctypes.c_void_p(dout.data_ptr()),
-                                                    _lib.ptr(dx), ctx.training, accumulate,
-                                                    _lib.stream_handle(dev)),
+            _lib.check(L.hcu_unet_backward(plan.handle, ctypes.byref(t),
+                                           ctypes.c_void_p(dout.data_ptr()),
+                                           _lib.ptr(dx), ctx.training, accumulate,
+                                           _lib.stream_handle(dev)),
                        'Unet_Constructor.backward')
         finish()
+        # in-place work on the gradients between here and allreduce_gradients
+        # (clip_grad_norm_, GradScaler.unscale_, .grad edits) bumps this
+        # version: the overlapped reduction then falls back to one collective
+        # behind the caller's stream (hcunet_amd/dist.py)
+        eng.grad_version = eng.grad_flat._version if G is eng.grad_flat else None
         if dx is not None and dx.dtype != x.dtype:
             dx = dx.to(x.dtype)
         return (dx, None, None, None) + (None,) * len(eng.params)

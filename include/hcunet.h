@@ -233,6 +233,10 @@ int hcu_gate_bwd(const float *hp, const float *zp, const float *h_prev, const fl
 /* costs one extra batched weight-gradient finalize launch.  NULL events:    */
 /* nothing recorded (the default).  The events stay owned by the caller.     */
 int hcu_unet_set_grad_events(hcu_unet_plan *plan, void *ev_decoder, void *ev_deep, int deep_level);
+/* 1 when hcu_unet_backward records those events (direct launches), 0 when  */
+/* its backward is replayed from a captured graph (HCU_GRAPHS=1), where a    */
+/* record would only be a capture dependency: reduce after the backward.     */
+int hcu_unet_grad_events_live(const hcu_unet_plan *plan);
 int hcu_event_create(void **ev);          /* hipEventDisableTiming */
 int hcu_event_destroy(void *ev);
 int hcu_stream_wait_event(hcu_stream_t stream, void *ev);

@@ -201,3 +201,59 @@ def test_reduction_in_ranges_equals_one_reduction():
     for r in (0, 1):
         np.testing.assert_array_equal(res[r][0], res[r][1])
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def _runet_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hcunet_amd.r_unet import RecursiveUnet
+        import hcunet_amd
+        torch.manual_seed(0)
+        m = RecursiveUnet(image_dimensions=3)
+        g = torch.Generator().manual_seed(100 + rank)
+        bns = [b for b in m.modules() if isinstance(b, torch.nn.BatchNorm3d)]
+        with torch.no_grad():
+            for b in bns:   # per-rank running statistics, as a per-shard forward leaves them
+                b.running_mean.copy_(torch.randn(b.running_mean.shape, generator=g))
+                b.running_var.copy_(torch.rand(b.running_var.shape, generator=g) + 0.5)
+            for p in m.parameters():
+                p.grad = torch.randn(p.shape, generator=g)
+        local = {k: v.clone().numpy() for k, v in m.state_dict().items() if 'running' in k}
+        lg = {n: p.grad.clone().numpy() for n, p in m.named_parameters()}
+        hcunet_amd.dist.allreduce_gradients(m)
+        q.put((rank, len(bns), local, lg,
+               {k: v.clone().numpy() for k, v in m.state_dict().items() if 'running' in k},
+               {n: p.grad.clone().numpy() for n, p in m.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_reduces_recursive_unet_batchnorm_statistics():
+    """Any module's BatchNorm running statistics join the reduction (not only
+    Unet_Constructor's): RecursiveUnet's 16 BatchNorm3d layers
+    (/root/reference/hcat/r_unet.py:276-277,326-327) stay rank-symmetric."""
+    import numpy as np
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_runet_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, *rest = q.get(timeout=300)
+        res[r] = rest
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (nbn, l0, g0, s0, r0), (_, l1, g1, s1, r1) = res[0], res[1]
+    assert nbn == 16   # fz / fh alias down2_*/down3_*/up1_*: state_dict repeats those keys
+    for k in s0:
+        np.testing.assert_array_equal(s0[k], s1[k])
+        np.testing.assert_allclose(s0[k], (l0[k] + l1[k]) / 2, rtol=1e-6, atol=1e-7, err_msg=k)
+    for n in r0:
+        np.testing.assert_array_equal(r0[n], r1[n])
+        np.testing.assert_allclose(r0[n], (g0[n] + g1[n]) / 2, rtol=1e-6, atol=1e-7, err_msg=n)

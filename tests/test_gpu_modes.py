@@ -70,14 +70,10 @@ def test_split_graphed_equals_serial(tmp_path):
     serial = _run(tmp_path, 'serial', {'HCU_SIDE': '0', 'HCU_GRAPHS': '0'})
     split = _run(tmp_path, 'split', {'HCU_SIDE': '1', 'HCU_GRAPHS': '1'})
     direct = _run(tmp_path, 'direct', {'HCU_SIDE': '1', 'HCU_GRAPHS': '0'})   # the default
-    # the opt-in forked weight re-layout in the training forward, and the
-    # branch ordered by marker events instead of chain-kernel stop events
-    fwdside = _run(tmp_path, 'fwdside', {'HCU_FWD_SIDE': '1', 'HCU_FORK_MARKERS': '1'})
     for it in range(3):
-        for a, b, d, f in zip(serial[it], split[it], direct[it], fwdside[it]):
+        for a, b, d in zip(serial[it], split[it], direct[it]):
             assert torch.equal(a, b)
             assert torch.equal(a, d)
-            assert torch.equal(a, f)
 
 
 def test_fused_bn_finalize_matches_separate(tmp_path):
