@@ -36,8 +36,9 @@ static void btile(int OX, int OY, int TZ, int maxM, int &TX, int &TY) {
 // floats of the halo image region: [HV] rows of ckp_bytes(CV) + a dummy 16-byte slot
 static long bconv_areg(const GConvArgs &a, int CV) {
   const long HV = (long)a.HX * a.HY * a.HZ;
-  // >= 4 waves x 64 columns x 3 floats: the statistics merge reuses the region
-  return std::max(768L, ((HV * ckp_bytes(CV) + 16) / 4 + 3) & ~3L);
+  // >= 4 waves x 64 columns x 3 floats: the statistics merge reuses the region;
+  // >= 512 doubles + a flag word: the BatchNorm-backward finalize tail does too
+  return std::max(1152L, ((HV * ckp_bytes(CV) + 16) / 4 + 3) & ~3L);
 }
 
 static long bconv_lds(const GConvArgs &a, int CV, int NT) {
@@ -45,7 +46,7 @@ static long bconv_lds(const GConvArgs &a, int CV, int NT) {
   const int TPS = 4 / CV;
   const int S = (T + TPS - 1) / TPS;
   return (bconv_areg(a, CV) + (long)S * 4 * NT * 4 + S * 4 + (long)a.MPW * 128 + 9L * NT +
-          2L * a.ICs) * 4 + (long)sizeof(GConvArgs);   // + the static copy of the arguments
+          3L * a.ICs) * 4 + (long)sizeof(GConvArgs);   // + the static copy of the arguments
 }
 
 int bconv_stat_rows(const GConvArgs &a) {

@@ -187,9 +187,33 @@ struct BnFin {
   int C, Cs, R, W;
   unsigned *counter;
 };
+// BatchNorm-backward finalize in the last workgroup of a kernel that writes
+// the (sum dz, sum dz*xhat) rows (the fused dgrad epilogue, the pool / dense
+// reductions, the out_conv backward): per column group g (the workgroups
+// sharing blockIdx.y) the workgroup taking the last ticket of counter[g]
+// sums the group's rows in fp64 in a fixed order and writes dbeta / dgamma
+// and the c1 / c0 coefficients of dy = dz*scale + c1*y + c0 (bn_bwd_finalize's
+// arithmetic), then resets counter[g] to 0.  counter == nullptr: no tail (the
+// separate bn_bwd_finalize launch).  The counters are zeroed once per call
+// (Ctx::counters) and the rows stored write-through (sc1).
+struct BnbFin {
+  float *dgamma, *dbeta;   // parameter gradients (nullable)
+  float *c1, *c0;          // [Cs] coefficients written
+  double count;            // elements per channel
+  int C;                   // real channels (c >= C get c1 = c0 = 0)
+  int training, accumulate;
+  unsigned *counter;       // [column groups] tickets
+};
 struct GConvArgs {
   const float *in;
   const float *in_scale, *in_shift;   // [ICs] or null
+  // Input gradient with the BatchNorm backward applied on load (AP instances,
+  // in_y != null): `in` holds dz of a BatchNorm layer whose pre-BN output is
+  // in_y (same layout), and the staged operand is dz*in_scale + (in_shift*y +
+  // in_c0) per channel (in_scale = BN scale, in_shift = c1, in_c0 = c0): the
+  // bits bn_bwd_apply would have stored.
+  const float *in_y, *in_c0;
+  BnbFin bfin;                        // BNB epilogue: finalize in the last workgroup
   const float *w;                     // [T][ICs][CoutW]
   const float *bias;                  // [Cout] or null
   float *out;
@@ -360,6 +384,91 @@ __device__ __forceinline__ bool bn_fin_ticket(unsigned *counter, int *flag_lds) 
 }
 __device__ __forceinline__ void bn_fin_reset(unsigned *counter) {
   __hip_atomic_store((hcu_gu32 *)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The same hand-off for the workgroups of one column group: nb tickets on
+// `counter` (BnbFin).  The rows must have been stored with st_sc1_f2.
+__device__ __forceinline__ bool bn_ticket_n(unsigned *counter, unsigned nb, int *flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add((hcu_gu32 *)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = t == nb - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  const bool last = *(volatile int *)flag_lds != 0;
+  __syncthreads();
+  if (last) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  return last;
+}
+__device__ __forceinline__ void st_sc1_f2(float *p, float2 v) {
+  const unsigned long long u = ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
+  __hip_atomic_store((hcu_gu64 *)p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// BatchNorm-backward finalize of channels cb .. cb+nc-1 from the R rows
+// [R][W][2] (sum dz, sum dz*xhat), by the workgroup that took the last ticket
+// (BnbFin).  TPC threads per channel sum strided rows in fp64 (eight loads in
+// flight), then a fixed-order tree: deterministic.  red: 512 doubles of LDS.
+// c1 / c0 are bn_bwd_finalize_kernel's (pointwise.hip) arithmetic.
+__device__ __forceinline__ void bnb_finalize_tail(const float *rows, int R, int W, int cb, int nc,
+                                                  const float *scale, const float *invstd,
+                                                  const float *mean, const BnbFin &f, double *red) {
+  const int tid = threadIdx.x;
+  int TPC = 1;
+  while (TPC * 2 * nc <= 256 && TPC < 64) TPC *= 2;
+  const int CPP = 256 / TPC, sub = tid % TPC;
+  for (int g0 = 0; g0 < nc; g0 += CPP) {
+    const int j = g0 + tid / TPC, c = cb + j;
+    double s1 = 0.0, s2 = 0.0;
+    if (j < nc) {
+      for (int r0 = sub; r0 < R; r0 += 8 * TPC) {
+        float2 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int r = r0 + u * TPC;
+          v[u] = r < R ? *reinterpret_cast<const float2 *>(rows + ((size_t)r * W + c) * 2)
+                       : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          s1 += (double)v[u].x;
+          s2 += (double)v[u].y;
+        }
+      }
+    }
+    __syncthreads();
+    red[tid] = s1;
+    red[256 + tid] = s2;
+    __syncthreads();
+    for (int off = TPC / 2; off > 0; off >>= 1) {
+      if (sub < off) {
+        red[tid] += red[tid + off];
+        red[256 + tid] += red[256 + tid + off];
+      }
+      __syncthreads();
+    }
+    if (sub == 0 && j < nc) {
+      const double db = red[tid], dg = red[256 + tid];
+      float c1v = 0.f, c0v = 0.f;
+      if (c < f.C) {
+        if (f.dbeta) f.dbeta[c] = f.accumulate ? f.dbeta[c] + (float)db : (float)db;
+        if (f.dgamma) f.dgamma[c] = f.accumulate ? f.dgamma[c] + (float)dg : (float)dg;
+        if (f.training) {
+          const double sc = scale[c], is = invstd[c], mu = mean[c];
+          const double c1 = -sc * is * dg / f.count;
+          c1v = (float)c1;
+          c0v = (float)(-sc * db / f.count - c1 * mu);
+        }
+      }
+      f.c1[c] = c1v;
+      f.c0[c] = c0v;
+    }
+  }
 }
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
 // (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n

@@ -433,6 +433,7 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 }  // namespace
 
 #define HCU_NBUF 32   // gradient slots (at most; Ctx::alloc)
+constexpr int kCtrPerSite = 64;   // BnbFin ticket counters per producing launch (column groups)
 #define HCU_NBUF_RING 6   // ring size when one slot per allocation does not fit
 #define HCU_FORK_RING 16   // marker events of forks that cannot use the chain record
 
@@ -468,7 +469,8 @@ struct hcu_unet_plan {
   int nbuf = HCU_NBUF_RING;
   bool no_reuse = false;
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
-  size_t fin_off = 0;   // fused BatchNorm finalize ticket counter (zeroed per forward)
+  size_t fin_off = 0;   // finalize ticket counters (HCU_BNFIN forward; BnbFin tails of the backward)
+  int n_ctr_sites = 0;  // BnbFin counter blocks (kCtrPerSite words each)
   double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
   // Layer-chain plans (hcu_chain_*): a sequence of ops instead of the U-Net.
   struct ChainOp {
@@ -793,7 +795,9 @@ int build_plan(hcu_unet_plan &p) {
   p.wpart_off = scratch.take_floats(p.wpart_floats);
   p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
-  p.fin_off = scratch.take_floats(16);
+  // one counter block per BatchNorm layer's backward finalize (+ slack)
+  p.n_ctr_sites = fwd_only ? 0 : p.n_bn + 4;
+  p.fin_off = scratch.take_floats(std::max<size_t>(16, (size_t)p.n_ctr_sites * kCtrPerSite));
   p.scratch_bytes = scratch.off;
   if (getenv("HCU_PLAN_LOG")) {   // weight-gradient kernels and their partial slabs (measurement)
     auto wlog = [](const std::string &n, const WGradArgs &w) {
@@ -859,6 +863,25 @@ struct Ctx {
     return 0;
   }
   float *wprep() const { return fptr(sc, p.wprep_off); }
+  // Ticket counters of the BatchNorm-backward finalize tails (BnbFin): one
+  // block of kCtrPerSite words per producing launch, all zeroed by one memset
+  // at the start of the backward (zero_counters) and left at zero by each
+  // launch's last workgroup.
+  int ctr_next = 0;
+  unsigned *counters(int n) {
+    if (n > kCtrPerSite || ctr_next >= p.n_ctr_sites) return nullptr;   // no tail: separate finalize
+    unsigned *r = reinterpret_cast<unsigned *>(sc + p.fin_off) + (size_t)ctr_next * kCtrPerSite;
+    ++ctr_next;
+    return r;
+  }
+  int zero_counters() {
+    if (p.n_ctr_sites) HCU_HIP(hipMemsetAsync(sc + p.fin_off, 0, (size_t)p.n_ctr_sites * kCtrPerSite * 4, s));
+    return 0;
+  }
+  // Layers whose dY = dz*scale + c1*y + c0 is not materialised: their
+  // consumers (weight and input gradient) apply it on load (ap_ok).
+  unsigned long long ap_mask = 0;
+  bool ap(const ConvLayer &L) const { return (ap_mask >> L.bn.index) & 1ull; }
   float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
   float *kpart() const { return fptr(sc, p.kpart_off); }
   hipStream_t wstream() const { return split ? ws : s; }
@@ -925,6 +948,19 @@ void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
 }
 
+// HCU_BNB_TAIL=0: the separate bn_bwd_finalize launch for every BatchNorm
+// backward instead of the last-workgroup finalize (BnbFin; A/B)
+bool tails_enabled() {
+  static const bool on = !(getenv("HCU_BNB_TAIL") && getenv("HCU_BNB_TAIL")[0] == '0');
+  return on;
+}
+
+// rows x channels a finalize tail may read (HCU_BNB_TAIL_MAX, A/B)
+long tail_max_values() {
+  static const long v = getenv("HCU_BNB_TAIL_MAX") ? atol(getenv("HCU_BNB_TAIL_MAX")) : 4096;
+  return v;
+}
+
 bool bnfin_enabled() {
   static const bool on = getenv("HCU_BNFIN") && getenv("HCU_BNFIN")[0] == '1';
   return on;
@@ -976,8 +1012,10 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
 
 // Sets up the dgrad epilogue that also performs the BatchNorm+ReLU backward
 // reduction of layer `bnl` (whose output the gradient is for); false when the
-// planned kernel cannot.
-bool fuse_bnbwd(const Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
+// planned kernel cannot.  When the kernel can also finalize in its last
+// workgroup (BnbFin: bconv, its K-split reduce) and a counter block is free,
+// the separate bn_bwd_finalize launch is dropped (finish_bnbwd).
+bool fuse_bnbwd(Ctx &c, GConvArgs &a, const ConvLayer *bnl, int training, int accumulate) {
   static const bool off = getenv("HCU_NO_BNFUSE") != nullptr;   // A/B debugging
   if (off || !bnl || !conv_bnbwd_fusable(a)) return false;
   const BNCoef coef = coef_at(c.sv, bnl->bn);
@@ -987,74 +1025,99 @@ bool fuse_bnbwd(const Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
   a.bn_mean = coef.mean;
   a.bn_invstd = coef.invstd;
   a.stats = c.part();
+  a.bfin = BnbFin{};
+  // The last workgroup reads every row of its column group: worth it (vs the
+  // separate finalize launch) only when that is a couple of loads per thread.
+  const int groups = a.ksplit > 1 ? 1 : a.CoutW / (a.NSUB * 16);
+  const long tail_vals = (long)gconv_rows(a) * (a.ksplit > 1 ? a.OCs : a.NSUB * 16);
+  if (a.use_bconv && tails_enabled() && tail_vals <= tail_max_values()) {
+    if (unsigned *ctr = c.counters(groups)) {
+      BnbFin &f = a.bfin;
+      f.dgamma = c.G + bnl->bn.gamma;
+      f.dbeta = c.G + bnl->bn.beta;
+      f.c1 = coef.c1;
+      f.c0 = coef.c0;
+      f.count = bnl->bn.count;
+      f.C = bnl->bn.C;
+      f.training = training;
+      f.accumulate = accumulate;
+      f.counter = ctr;
+    }
+  }
   return true;
 }
 
-// Finalize + apply of a BatchNorm backward whose reduction ran in a dgrad epilogue.
-// BatchNorm-backward finalize + apply: two launches; HCU_BNFA=1 fuses them
-// for layers with few partial rows (launch_bn_bwd_finalize_apply) -- measured
-// equal within noise on MI355X, so the simpler form stays the default.
-static int bn_fin_apply(const float *part, int R, int W, const BNLayer &bn, BNCoef coef, float *G,
-                        int training, int accumulate, float *dz, const float *y, int64_t nvox, int Cs,
-                        hipStream_t s, int bf, bool apply = true) {
-  static const bool sep = !(getenv("HCU_BNFA") && getenv("HCU_BNFA")[0] == '1');
-  if (!apply)   // the consumer applies dz*scale + c1*y + c0 on load (WGradArgs::g_y)
-    return launch_bn_bwd_finalize(part, R, bn.C, bn.Cs, W, bn.count, coef, G + bn.gamma, G + bn.beta,
-                                  training, accumulate, s);
-  if (sep) {
-    if (int e = launch_bn_bwd_finalize(part, R, bn.C, bn.Cs, W, bn.count, coef, G + bn.gamma, G + bn.beta,
-                                       training, accumulate, s))
+// Finalize (unless the producing kernel did it in its last workgroup) and
+// apply (unless bnl's consumers apply it on load, Ctx::ap) of a BatchNorm
+// backward whose reduction rows are in c.part().
+int finish_bn(const Ctx &c, const ConvLayer &bnl, int R, int W, bool tail_done, float *dz, int training,
+              int accumulate) {
+  const BNCoef coef = coef_at(c.sv, bnl.bn);
+  if (!tail_done)
+    if (int e = launch_bn_bwd_finalize(c.part(), R, bnl.bn.C, bnl.bn.Cs, W, bnl.bn.count, coef,
+                                       c.G + bnl.bn.gamma, c.G + bnl.bn.beta, training, accumulate, c.s))
       return e;
-    return launch_bn_bwd_apply(dz, y, coef, nvox, Cs, s, bf);
-  }
-  return launch_bn_bwd_finalize_apply(part, R, W, bn.C, bn.Cs, bn.count, coef, G + bn.gamma, G + bn.beta,
-                                      training, accumulate, dz, y, nvox, s, bf);
+  if (c.ap(bnl)) return 0;
+  return launch_bn_bwd_apply(dz, c.fptr(c.sv, bnl.y_off), coef, bnl.out.vox(), bnl.out.Cs, c.s, c.bf());
 }
 
 int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *dz, int training,
-                 int accumulate, bool apply = true) {
-  const BNCoef coef = coef_at(c.sv, bnl.bn);
-  return bn_fin_apply(c.part(), gconv_rows(a), a.CoutW, bnl.bn, coef, c.G, training, accumulate, dz,
-                      c.fptr(c.sv, bnl.y_off), bnl.out.vox(), bnl.out.Cs, c.s, c.bf(), apply);
+                 int accumulate) {
+  return finish_bn(c, bnl, gconv_rows(a), a.CoutW, a.bfin.counter != nullptr, dz, training, accumulate);
 }
 
-// The layer's weight gradient can take its gradient operand as d(post-BN) dz
-// and apply the BatchNorm backward on load (wgrad8 form 0 fp32, pipelined
-// bwgrad bf16): used when
-// that weight gradient is the apply's only consumer (the first layer, no
-// input gradient), which removes a full read-modify-write pass of the
-// largest gradient tensor from the end of the backward.
-bool gap_ok(const Ctx &c, const ConvLayer &L) {
-  static const bool off = getenv("HCU_NO_GAP") && getenv("HCU_NO_GAP")[0] == '1';   // A/B
-  if (off) return false;
-  // bf16: opt-in (HCU_GAP_BF16=1).  Measured on MI355X (config 3, d0.c1): the
-  // pipelined bwgrad with the operand apply ran 253 us against 115 + 116 us for
-  // bwgrad + the separate apply (register pressure of the second operand)
-  static const bool bf_on = getenv("HCU_GAP_BF16") && getenv("HCU_GAP_BF16")[0] == '1';
-  if (c.bf()) return bf_on && bwgrad_gap_ok(L.wg);
-  return L.wg.v2 == 2 && L.wg.w8mode == 0 && L.wg.GCs <= 16;
+// Whether layer L's consumers -- its weight gradient and, when planned, its
+// input gradient -- can apply the BatchNorm backward on load (dz*scale +
+// c1*y + c0 while staging the operand), so dY(L) is never materialised: the
+// input gradient on bconv (AP instances), the weight gradient on wgrad2,
+// wgrad8 form 0 or the pipelined bwgrad.  HCU_AP=0 materialises every dY
+// (the bn_bwd_apply pass, A/B); HCU_AP_BF16=0 only the bf16 ones.
+bool ap_ok(const Ctx &c, const ConvLayer &L, bool with_dgrad) {
+  static const bool on = !(getenv("HCU_AP") && getenv("HCU_AP")[0] == '0');
+  static const bool bf_on = !(getenv("HCU_AP_BF16") && getenv("HCU_AP_BF16")[0] == '0');
+  // Measured on MI355X (config 2): a consumer staging dz and y runs 15-40 %
+  // longer on a large layer (d1/d2: two HBM operand streams), which costs more
+  // than the apply pass it removes; on the small deep layers the launch saved
+  // dominates.  HCU_AP_MAX_MB: the largest dY (MB) applied on load.
+  static const double max_b = 1e6 * (getenv("HCU_AP_MAX_MB") ? atof(getenv("HCU_AP_MAX_MB")) : 8.0);
+  if (!on || c.p.is_chain || L.bn.index >= 64) return false;
+  const bool small = (double)L.out.vox() * L.out.Cs * L.out.es <= max_b;
+  if (with_dgrad && (!small || !L.dgrad.use_bconv)) return false;
+  const WGradArgs &w = L.wg;
+  // (the bf16 first layer's bwgrad with the operand apply ran 253 us against
+  // 115 + 116 for bwgrad + the apply pass: only small bf16 layers)
+  if (w.use_bw) return bf_on && small && bwgrad_gap_ok(w);
+  // wgrad8 form 0: the fp32 first layer (no input gradient) applies on load
+  // at any size (round 3: the 31 us apply pass gone from the chain's end)
+  if (w.v2 == 2) return w.w8mode == 0 && w.GCs <= 16 && (small || !with_dgrad);
+  return w.v2 == 1 && small;
+}
+// Decides (once, before dz(L) is produced) whether L's dY stays unmaterialised.
+void decide_ap(Ctx &c, const ConvLayer &L, bool with_dgrad) {
+  if (ap_ok(c, L, with_dgrad)) c.ap_mask |= 1ull << L.bn.index;
 }
 
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
-// With `bnl`, the input gradient leaves as d(pre-BN y) of layer bnl (its
+// dy holds dY of L, or dz of L when Ctx::ap(L) (applied on load by both
+// consumers).  With `bnl`, the input gradient leaves as dz of layer bnl (its
 // BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
-                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr,
-                  bool defer_apply = false, const ConvLayer *gap = nullptr) {
+                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
+  const bool ap = c.ap(L);
+  const BNCoef lc = coef_at(c.sv, L.bn);
   WGradArgs w = L.wg;
   w.A = A;
   w.a_scale = asc;
   w.a_shift = ash;
   w.G = dy;
-  if (gap) {   // dy holds dz of gap's BatchNorm: applied on load
-    const BNCoef gc = coef_at(c.sv, gap->bn);
-    w.g_y = c.fptr(c.sv, gap->y_off);
-    w.g_scale = gc.scale;
-    w.g_c1 = gc.c1;
-    w.g_c0 = gc.c0;
+  if (ap) {   // dy holds dz of L's BatchNorm: applied on load
+    w.g_y = c.fptr(c.sv, L.y_off);
+    w.g_scale = lc.scale;
+    w.g_c1 = lc.c1;
+    w.g_c0 = lc.c0;
   }
   if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
   if (int e = launch_wgrad(w, c.wstream())) return e;
@@ -1079,21 +1142,27 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   tag(L.name, "dgrad");
   GConvArgs a = L.dgrad;
   a.in = dy;
+  if (ap) {
+    a.in_y = c.fptr(c.sv, L.y_off);
+    a.in_scale = lc.scale;
+    a.in_shift = lc.c1;
+    a.in_c0 = lc.c0;
+  }
   a.w = c.fptr(c.sv, L.wd_off);
   a.out = dA;
   a.partial = c.kpart();
-  const bool fused = fuse_bnbwd(c, a, bnl);
+  const bool fused = fuse_bnbwd(c, a, bnl, training, accumulate);
   if (int e = launch_conv_any(a, c.s)) return e;
   if (!fused) return 0;
   tag(bnl->name, "bnbwd");
-  if (int e = finish_bnbwd(c, a, *bnl, dA, training, accumulate, !defer_apply)) return e;
+  if (int e = finish_bnbwd(c, a, *bnl, dA, training, accumulate)) return e;
   if (bn_done) *bn_done = true;
   return 0;
 }
 
 // BatchNorm+ReLU backward for layer L: dbuf holds d(post-activation) on entry
-// and d(pre-BN y) on exit (unless pool_dP is given, in which case dbuf is
-// produced from the max-pool gradient).
+// and dz (Ctx::ap(L)) or d(pre-BN y) on exit (unless pool_dP is given, in
+// which case dbuf is produced from the max-pool gradient).
 int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool_dP,
                 const int *pool_k, int training, int accumulate) {
   tag(L.name, "bnbwd");
@@ -1111,8 +1180,7 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
                                            c.bf()))
       return e;
   }
-  return bn_fin_apply(c.part(), R, L.bn.Cs, L.bn, coef, c.G, training, accumulate, dbuf, y, nvox,
-                      L.out.Cs, c.s, c.bf());
+  return finish_bn(c, L, R, L.bn.Cs, false, dbuf, training, accumulate);
 }
 
 }  // namespace
@@ -1467,12 +1535,14 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(),
                                 c.s))
       return e;
-  int cur = 0;  // slot holding the current d(pre-BN y)
+  if (int e = c.zero_counters()) return e;
+  int cur = 0;  // slot holding the current d(pre-BN y) (or dz, Ctx::ap)
   if (int e = c.alloc(cur)) return e;
 
   // out_conv + last BatchNorm
   const ConvLayer &last = p.uc2[p.L - 2];
   tag(std::string("out"), "bwd");
+  decide_ap(c, last, true);
   {
     const BNCoef coef = coef_at(c.sv, last.bn);
     const int64_t nvox = last.out.vox();
@@ -1486,9 +1556,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = launch_outconv_wfinalize(part_oc, R, p.Co, last.out.C, last.out.Cs, c.G + p.oc_w,
                                          c.G + p.oc_b, accumulate, c.s))
       return e;
-    if (int e = bn_fin_apply(part_bn, R, last.bn.Cs, last.bn, coef, c.G, training, accumulate,
-                             c.buf(cur), c.fptr(c.sv, last.y_off), nvox, last.out.Cs, c.s, c.bf()))
-      return e;
+    if (int e = finish_bn(c, last, R, last.bn.Cs, false, c.buf(cur), training, accumulate)) return e;
   }
   // decoder, last to first
   for (int j = p.L - 2; j >= 0; --j) {
@@ -1501,6 +1569,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.alloc(sb)) return e;
     float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
+    decide_ap(c, c1, true);
     if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
                               accumulate, &c1, training, &done1))
       return e;
@@ -1565,7 +1634,8 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       a.w = c.fptr(c.sv, u.wd_off);
       a.out = dP;
       a.partial = c.kpart();
-      const bool fused = fuse_bnbwd(c, a, &prev);
+      decide_ap(c, prev, true);
+      const bool fused = fuse_bnbwd(c, a, &prev, training, accumulate);
       if (int e = launch_conv_any(a, c.s)) return e;
       if (fused) {
         tag(prev.name, "bnbwd");
@@ -1597,11 +1667,11 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.alloc(sb)) return e;
     float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
-    // first layer without an input gradient: its weight gradient is the only
-    // consumer of d(pre-BN y1) and applies the BatchNorm backward on load
-    const bool gap = i == 0 && !dx && gap_ok(c, c1);
+    // (the first layer without an input gradient: its weight gradient is the
+    // only consumer of dz(y1))
+    decide_ap(c, c1, i > 0 || dx);
     if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
-                              accumulate, &c1, training, &done1, gap))
+                              accumulate, &c1, training, &done1))
       return e;
     if (!done1)
       if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
@@ -1611,13 +1681,13 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.alloc(sa)) return e;
       dIn = c.buf(sa);
     }
-    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training,
-                              nullptr, false, gap && done1 ? &c1 : nullptr))
+    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training))
       return e;
     if (i > 0) {
       // dIn = d(pooled): produce d(pre-BN y2_{i-1}) into a fresh slot
       int sp = 0;
       if (int e = c.alloc(sp)) return e;
+      decide_ap(c, p.dc2[i - 1], true);
       if (int e = bn_backward(c, p.dc2[i - 1], c.buf(sp), dIn, s.pool_k, training, accumulate))
         return e;
       cur = sp;
@@ -2411,7 +2481,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       g.out = dP;
       g.partial = c.kpart();
       const ConvLayer *bnl = (pr && pr->kind == HCU_CHAIN_CONV && pr->bn_relu) ? &pr->conv : nullptr;
-      const bool fused = fuse_bnbwd(c, g, bnl);
+      const bool fused = fuse_bnbwd(c, g, bnl, training, accumulate);
       if (int e = launch_conv_any(g, s)) return e;
       if (fused)
         if (int e = finish_bnbwd(c, g, *bnl, dP, training, accumulate)) return e;
