@@ -591,6 +591,13 @@ struct WGradArgs {
   // BN) dz and the operand is dz*g_scale + (g_c1*g_y + g_c0) per channel, the
   // bits bn_bwd_apply would have stored; null: G is the operand itself.
   const float *g_y, *g_scale, *g_c1, *g_c0;
+  // ConvTranspose3d with kernel % stride == 0 as the weight gradient of its
+  // phase-folded forward convolution (wgrad2, taps_rows): rows (j, ci) over
+  // the J = K / S taps with A zero-padded by J - 1 (apx..), columns (phase q,
+  // co) with q = (qx*phy + qy)*phz + qz, G read at o*S + q (gsx = S): the
+  // stride phases are extra output columns and the bias row sums dU per
+  // (q, co) -- no separate chansum.  nph <= 1: plain Conv3d form.
+  int nph, phx, phy, phz, GCout;
 };
 int plan_bwgrad(WGradArgs &a, int target_blocks);
 int launch_bwgrad(const WGradArgs &a, hipStream_t s);
@@ -612,9 +619,12 @@ struct WGradFinalize {
   const float *partial;
   float *dw, *db;
   int KB, Mtot, Ntot, T;
-  int mode;   // 0 Conv3d (taps rows), 1 ConvTranspose3d, 2 bias column sums (db[c < Cout])
+  int mode;   // 0 Conv3d (taps rows), 1 ConvTranspose3d, 2 bias column sums (db[c < Cout]),
+              // 3 ConvTranspose3d in the phase form (WGradArgs::nph): row (j, ci), column
+              // (q, co) -> dW[ci][co][t], t = (J-1-j)*S + q per dimension; db[co] = sum_q bias row
   int Cout, Cin_g, groups, fold_mod, ACs;   // conv
   int Cin, CoutT, GCs;                      // convT
+  int J[3], SS[3];                          // mode 3: taps per phase, stride
   int accumulate;
 };
 int launch_wgrad_finalize(const WGradFinalize &f, hipStream_t s);
@@ -817,7 +827,9 @@ int launch_prep_convt_dgrad(const float *w, float *wg, int Cin, int Cout, int T,
 enum PrepKind { PREP_CONV_FWD = 0, PREP_CONV_DGRAD = 1, PREP_CONVT_FUSED = 2,
                 PREP_CONVT_PHASE = 3, PREP_CONVT_DGRAD = 4 };
 struct PrepJob {
-  int kind, bf16;   // bf16 != 0: the prepared image is written as bf16 (bconv)
+  int kind;
+  short bf16;       // != 0: the prepared image is written as bf16 (bconv)
+  short tiled;      // set by launch_prep_all: the LDS-staged form (prep_all.hip)
   int64_t n;        // elements of the prepared buffer
   int64_t src;      // float offset of the PyTorch-layout weight in the parameter buffer
   int64_t dst;      // float offset of the prepared buffer in the destination workspace

@@ -118,6 +118,11 @@ struct ConvTLayer {
   GConvArgs fwdf{};
   GConvArgs dgrad{};
   WGradArgs wg{};
+  // the weight gradient of the phase-folded forward (WGradArgs::nph: phases
+  // as extra columns, the bias from its ones row -- no chansum), fp32 U-Net
+  // decoders with kernel % stride == 0 and Cout % 4 == 0
+  WGradArgs wgp{};
+  bool wg_phase = false;
   size_t u_off = 0;
   size_t wf_off = 0, wd_off = 0;   // prepared weights in `saved` (fused fwd, dgrad)
   std::vector<size_t> wph_off;     // per-phase fwd weights when not fused
@@ -426,6 +431,34 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     u.wg = w;
     max_part = std::max(max_part, wgrad_partial_floats(w));
     max_part = std::max(max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
+  }
+  u.wg_phase = false;
+  static const bool phase_on = !(getenv("HCU_CONVT_PHASE_WG") && getenv("HCU_CONVT_PHASE_WG")[0] == '0');
+  if (!bf && u.fused && o % 4 == 0 && phase_on) {
+    // dW'[(j, ci)][(q, co)] = sum_o A[o + j - (J-1)][ci] * dU[o*S + q][co] over the
+    // phase grid o (the forward's fused GEMM, hcat/unet.py:294-298)
+    const int J[3] = {u.K[0] / u.S[0], u.K[1] / u.S[1], u.K[2] / u.S[2]};
+    WGradArgs w{};
+    w.B = cur.B;
+    w.AX = cur.X; w.AY = cur.Y; w.AZ = cur.Z; w.ACs = cur.Cs;
+    w.GX = ux; w.GY = uy; w.GZ = uz; w.GCs = u.out.Cs;
+    w.PX = cur.X + J[0] - 1; w.PY = cur.Y + J[1] - 1; w.PZ = cur.Z + J[2] - 1;
+    w.KX = J[0]; w.KY = J[1]; w.KZ = J[2];
+    w.asx = w.asy = w.asz = 1;
+    w.adx = w.ady = w.adz = 1;
+    w.apx = J[0] - 1; w.apy = J[1] - 1; w.apz = J[2] - 1;
+    w.gsx = u.S[0]; w.gsy = u.S[1]; w.gsz = u.S[2];
+    w.gdx = w.gdy = w.gdz = 1;
+    w.taps_rows = 1;
+    w.bias_row = 1;
+    w.nph = nph; w.phx = u.S[0]; w.phy = u.S[1]; w.phz = u.S[2]; w.GCout = o;
+    if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == 1) {
+      u.wgp = w;
+      u.wg_phase = true;
+      max_part = std::max(max_part, wgrad_partial_floats(w));
+    } else {
+      set_error("");
+    }
   }
   return 0;
 }
@@ -807,7 +840,7 @@ int build_plan(hcu_unet_plan &p) {
     };
     for (const auto *v : {&p.dc1, &p.dc2, &p.uc1, &p.uc2})
       for (const ConvLayer &cl : *v) wlog(cl.name, cl.wg);
-    for (const ConvTLayer &u : p.up) wlog(u.name, u.wg);
+    for (const ConvTLayer &u : p.up) wlog(u.name, u.wg_phase ? u.wgp : u.wg);
   }
   return 0;
 }
@@ -1584,6 +1617,34 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     const BNCoef bp = coef_at(c.sv, prev.bn);
     tag(u.name, "wgrad");
     if (int e = c.fork()) return e;
+    if (u.wg_phase) {   // weight and bias gradient in one launch (WGradArgs::nph)
+      WGradArgs w = u.wgp;
+      w.A = c.fptr(c.sv, prev.y_off);
+      w.a_scale = bp.scale;
+      w.a_shift = bp.shift;
+      w.G = dU;
+      if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
+      if (int e = launch_wgrad(w, c.wstream())) return e;
+      WGradFinalize f{};
+      f.partial = w.partial;
+      f.dw = c.G + u.w_off;
+      f.db = c.G + u.b_off;
+      f.KB = w.KB;
+      f.Mtot = w.Mtot;
+      f.Ntot = w.Ntot;
+      f.T = u.T;
+      f.mode = 3;
+      f.Cin = u.Cin;
+      f.CoutT = u.Cout;
+      f.ACs = w.ACs;
+      f.GCs = w.GCs;
+      for (int d = 0; d < 3; ++d) {
+        f.J[d] = u.K[d] / u.S[d];
+        f.SS[d] = u.S[d];
+      }
+      f.accumulate = accumulate;
+      if (int e = c.pend_wgf(f)) return e;
+    } else {
     {
       const int R = chansum_rows(u.out.vox(), u.out.Cs);
       float *cs = nullptr;
@@ -1623,6 +1684,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       f.GCs = w.GCs;
       f.accumulate = accumulate;
       if (int e = c.pend_wgf(f)) return e;
+    }
     }
     if (int e = c.read_done(su)) return e;
     tag(u.name, "dgrad");

@@ -297,7 +297,17 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
 #pragma unroll
   for (int ns = 0; ns < NS; ++ns) {
     const int lc = ns * 16 + r16;
-    goff[ns] = (lc < CKG && co0 + lc < a.GCs) ? lc * PG : CKG * PG;
+    goff[ns] = (lc < CKG && co0 + lc < a.Ntot) ? lc * PG : CKG * PG;
+  }
+  // G channel base and stride phase of this block's columns (phase form: the
+  // chunk lies in one phase; else phase 0, columns = channels)
+  int gq[3] = {0, 0, 0}, gcb = co0;
+  if (a.nph > 1) {
+    const int q = co0 / a.GCout;
+    gcb = co0 - q * a.GCout;
+    gq[2] = q % a.phz;
+    gq[1] = (q / a.phz) % a.phy;
+    gq[0] = q / (a.phz * a.phy);
   }
 
   floatx4 acc[MS][NS];
@@ -337,9 +347,10 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
           a.fHAZ.divmod(v, q, hz);
           a.fHAY.divmod(q, hx, hy);
           vv[u] = (((hx << 10) | hy) << 10 | hz) * 8 + c4;  // c4 < 8
-          const int gx = px0 + hx, gy = py0 + hy, gz = pz0 + hz;
+          const int gx = px0 + hx - a.apx, gy = py0 + hy - a.apy, gz = pz0 + hz - a.apz;
           const int c = ci0 + c4 * 4;
-          if (gx < a.AX && gy < a.AY && gz < a.AZ && c < a.ACs) {
+          if ((unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY && (unsigned)gz < (unsigned)a.AZ &&
+              c < a.ACs) {
             val[u] = *reinterpret_cast<const float4 *>(
                 a.A + ((((size_t)b * a.AX + gx) * a.AY + gy) * a.AZ + gz) * a.ACs + c);
             if (a.a_scale) {
@@ -385,9 +396,10 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
           a.fTY.divmod(q, lx, ly);
           pp[u] = ((lx * a.TY + ly) * TZP + lz) * 32 + c4;  // c4 < 32
           const int gx = px0 + lx, gy = py0 + ly, gz = pz0 + lz;
-          const int c = co0 + c4 * 4;
-          if (gx < a.PX && gy < a.PY && gz < a.PZ && c < a.GCs) {
-            const size_t go = ((((size_t)b * a.GX + gx) * a.GY + gy) * a.GZ + gz) * a.GCs + c;
+          const int c = gcb + c4 * 4;
+          if (gx < a.PX && gy < a.PY && gz < a.PZ && c < a.GCs && co0 + c4 * 4 < a.Ntot) {
+            const size_t go = ((((size_t)b * a.GX + gx * a.gsx + gq[0]) * a.GY + gy * a.gsy + gq[1]) * a.GZ +
+                               gz * a.gsz + gq[2]) * a.GCs + c;
             val[u] = *reinterpret_cast<const float4 *>(a.G + go);
             if (a.g_y) {   // G holds dz: the BatchNorm backward applied on load (bn_bwd_apply's bits)
               const float4 yv = *reinterpret_cast<const float4 *>(a.g_y + go);
@@ -469,7 +481,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
     } else if (bias_block && lr == a.TA * CKA) {
       grow = T * a.ACs;
     }
-    if (lc < CKG && co0 + lc < a.GCs) gcol = co0 + lc;
+    if (lc < CKG && co0 + lc < a.Ntot) gcol = co0 + lc;
     if (grow >= 0 && gcol >= 0)
       a.partial[((size_t)kb * a.Mtot + grow) * a.Ntot + gcol] = red[idx];
   }
@@ -479,8 +491,10 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
 // tile, padded LDS images, persistent grid.  Returns 0 when wgrad2 applies.
 static int plan_wgrad2(WGradArgs &a, int target_blocks) {
   a.v2 = 0;
-  if (!a.taps_rows || a.asx != 1 || a.asy != 1 || a.asz != 1 || a.gsx != 1 || a.gsy != 1 ||
-      a.gsz != 1 || a.apx || a.apy || a.apz || a.gpx || a.gpy || a.gpz)
+  // (the ConvTranspose3d phase form: A zero-padded, G strided by the phases)
+  const bool ph = a.nph > 1;
+  if (!a.taps_rows || a.asx != 1 || a.asy != 1 || a.asz != 1 || a.gpx || a.gpy || a.gpz ||
+      (!ph && (a.gsx != 1 || a.gsy != 1 || a.gsz != 1 || a.apx || a.apy || a.apz)))
     return 1;
   if (a.CKA % 4 || a.CKA > 32 || a.CKG > 128) return 1;
   const int ntz = cdiv(a.PZ, 16);
@@ -559,10 +573,17 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
         ta = (rows - brow) / 4;
       }
       cka = std::min(cka, a.ACs);
+      if (a.nph > 1) cka = std::min(cka, 32);   // wgrad2's A images: at most 32 channels a block
       a.CKA = cka;
       a.TA = ta;
       a.TG = 1;
       a.CKG = std::min(a.GCs, cols);
+      if (a.nph > 1) {   // column chunks inside one phase: CKG divides GCout
+        int ckg = std::min(a.GCout, cols) / 4 * 4;
+        while (ckg > 4 && a.GCout % ckg) ckg -= 4;
+        if (ckg < 4 || a.GCout % ckg) return fail(4, "wgrad: phase columns need Cout % 4 == 0");
+        a.CKG = ckg;
+      }
       a.mloc = ta * cka + brow;
       a.nloc = a.CKG;
     } else {
@@ -586,12 +607,13 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   }
   if (!a.NS) return fail(4, "wgrad: no tile");
   a.nci = cdiv(a.ACs, a.CKA);
-  a.nco = cdiv(a.GCs, a.CKG);
+  const int ncols = a.nph > 1 ? a.nph * a.GCout : a.GCs;   // taps_rows columns
+  a.nco = cdiv(ncols, a.CKG);
   a.ntc = a.taps_rows ? cdiv(T, a.TA) : cdiv(T, a.TG);
   a.mchunks = a.taps_rows ? a.ntc * a.nci : a.nci;
   a.nchunks = a.taps_rows ? a.nco : a.ntc * a.nco;
   a.Mtot = a.taps_rows ? T * a.ACs + (a.bias_row ? 1 : 0) : a.ACs;
-  a.Ntot = a.taps_rows ? a.GCs : T * a.GCs;
+  a.Ntot = a.taps_rows ? ncols : T * a.GCs;
   const int ntz = cdiv(a.PZ, 16);
   a.TZ = cdiv(a.PZ, ntz);
   int txy = std::max(1, 256 / a.TZ);
@@ -636,6 +658,11 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   long kb = std::max(1L, (long)target_blocks / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
+  if (a.nph > 1) {   // the phase form runs on wgrad2 only
+    if (wgrad2_disabled() || plan_wgrad2(a, target_blocks) != 0)
+      return fail(4, "wgrad: no wgrad2 tile for the ConvTranspose3d phase form");
+    return 0;
+  }
   if (plan_wgrad8(a) != 0 && !wgrad2_disabled()) plan_wgrad2(a, target_blocks);
   return 0;
 }
@@ -730,6 +757,37 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
   for (int j = 1; j < S; ++j) s += red[j * EPB + el];
   const float v = (float)s;
   const int grow = (int)(idx / f.Ntot), gcol = (int)(idx % f.Ntot);
+  if (f.mode == 3) {   // ConvTranspose3d, phase form (WGradArgs::nph)
+    const int Jt = f.J[0] * f.J[1] * f.J[2];
+    const int ph = gcol / f.CoutT, co = gcol % f.CoutT;
+    if (grow == Jt * f.ACs) {   // bias: the phase-0 thread sums every phase's column, in order
+      if (ph != 0 || !f.db) return;
+      const int nph = f.Ntot / f.CoutT;
+      double sb = s;
+      const int64_t brow = (int64_t)grow * f.Ntot;
+      for (int q = 1; q < nph; ++q) {
+        const float *src = f.partial + brow + q * f.CoutT + co;
+        double a2 = 0.0;
+        for (int k = 0; k < f.KB; ++k) a2 += (double)src[(size_t)k * n];
+        sb += a2;
+      }
+      const float vb = (float)sb;
+      f.db[co] = f.accumulate ? f.db[co] + vb : vb;
+      return;
+    }
+    const int j = grow / f.ACs, ci = grow % f.ACs;
+    if (ci >= f.Cin) return;
+    const int jz = j % f.J[2], jy = (j / f.J[2]) % f.J[1], jx = j / (f.J[2] * f.J[1]);
+    const int phz = f.SS[2], phy = f.SS[1];
+    const int qz = ph % phz, qy = (ph / phz) % phy, qx = ph / (phz * phy);
+    const int tx = (f.J[0] - 1 - jx) * f.SS[0] + qx, ty = (f.J[1] - 1 - jy) * f.SS[1] + qy,
+              tz = (f.J[2] - 1 - jz) * f.SS[2] + qz;
+    const int KY = f.J[1] * f.SS[1], KZ = f.J[2] * f.SS[2];
+    const int t = (tx * KY + ty) * KZ + tz;
+    float *dst = f.dw + ((size_t)ci * f.CoutT + co) * f.T + t;
+    *dst = f.accumulate ? *dst + v : v;
+    return;
+  }
   if (f.mode == 2) {   // column sums of R rows (ConvTranspose bias: rows = chansum partials)
     if (gcol < f.Cout && f.db) f.db[gcol] = f.accumulate ? f.db[gcol] + v : v;
     return;

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r'''
-import sys, torch
+import os, sys, torch
 sys.path.insert(0, %(root)r)
 from hcat.unet import Unet_Constructor
 from hcat.loss import cross_entropy
@@ -32,7 +32,8 @@ res = []
 for it in range(3):          # 3 steps: the graphed mode replays its capture
     for p in m.parameters():
         p.grad = None
-    out = m(x)
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=os.environ.get('HCU_TEST_BF16') == '1'):
+        out = m(x)
     ms = (x.shape[0], 1) + tuple(out.shape[2:])
     loss = cross_entropy(out, torch.from_numpy(inputs.make_mask(ms)).cuda(),
                          torch.from_numpy(inputs.make_pwl(ms)).cuda(), method='pixel')
@@ -142,3 +143,15 @@ def test_tiled_weight_gradient_finalize(tmp_path):
             assert torch.equal(b, c)
             tol = 2.5e-7 * max(a.abs().max().item(), 1e-30)
             assert (a - b).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize('bf16', ['0', '1'])
+def test_tiled_weight_relayout_matches_gather(tmp_path, bf16):
+    """The LDS-staged weight re-layout (prep_all.hip prep_tile) writes the
+    same packed images as the gather form: training steps bitwise equal, fp32
+    and bf16, including the decoder's cat-folded images."""
+    a = _run(tmp_path, 'gather' + bf16, {'HCU_PREP_TILED': '0', 'HCU_TEST_BF16': bf16})
+    b = _run(tmp_path, 'tiled' + bf16, {'HCU_PREP_TILED': '1', 'HCU_TEST_BF16': bf16})
+    for it in range(3):
+        for x, y in zip(a[it], b[it]):
+            assert torch.equal(x, y)

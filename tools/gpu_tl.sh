@@ -17,6 +17,6 @@ for arm in "$@"; do
     || { tail -20 $O/${TAG}_tl$k.log; exit 1; }
   for kv in $arm; do unset "${kv%%=*}"; done
   db=$(find $O/${TAG}_tl$k -name '*.db' | head -1)
-  python3 tools/timeline.py "$db" > $O/${TAG}_timeline$k.txt 2>&1 || true
+  python3 tools/timeline.py "$db" --all > $O/${TAG}_timeline$k.txt 2>&1 || true
   echo "arm $k [$arm]: $(head -1 $O/${TAG}_timeline$k.txt)"
 done

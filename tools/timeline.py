@@ -34,6 +34,7 @@ def main():
     ap.add_argument('db', nargs='+')
     ap.add_argument('--marker', default='adam_kernel')
     ap.add_argument('--gaps', type=int, default=25)
+    ap.add_argument('--all', action='store_true', help='every kernel of the step, all queues, by start')
     a = ap.parse_args()
     dbs = []
     for d in a.db:
@@ -98,6 +99,12 @@ def main():
               % (sum(e_ - s_ for s_, e_, _ in mb) / 1e3, (max(e_ for _, e_, _ in mb) - bwd0) / 1e3 if mb else 0,
                  sum(e_ - s_ for s_, e_, _ in side_ev) / 1e3, (max(e_ for _, e_, _ in side_ev) - bwd0) / 1e3,
                  (max(s_ for s_, _, n in main_ev if 'adam' in n) - bwd0) / 1e3))
+    if a.all:
+        qn = {q: i for i, q in enumerate(sorted(queues, key=lambda q: -len(queues[q])))}
+        print('\nall kernels (queue index, start offset us, end offset us, duration us):')
+        for n, s, e, q in sorted(step, key=lambda r: r[1]):
+            print('  q%d %8.1f %8.1f %7.1f  %s' % (qn[q], (s - t0) / 1e3, (e - t0) / 1e3, (e - s) / 1e3, short(n)))
+        return
     print('\ncritical-queue sequence (us: start offset, duration):')
     for n, s, e in ks:
         print('  %8.1f %7.1f  %s' % ((s - t0) / 1e3, (e - s) / 1e3, short(n)))
