@@ -142,9 +142,10 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
   const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
 
   // contiguous tile range per block (consecutive tiles share halo rows in L2)
-  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t_end = min(total, (int)blockIdx.x * tpb_ + tpb_);
-  for (int tt = blockIdx.x * tpb_; tt < t_end; ++tt) {
+  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int tpb_ = (total + KBt - 1) / KBt;
+  const int t_end = min(total, kbi * tpb_ + tpb_);
+  for (int tt = kbi * tpb_; tt < t_end; ++tt) {
     const int b = tt / ntiles;
     int tile = tt - b * ntiles;
     const int tzi = tile % a.ntz;
@@ -254,7 +255,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
   }
 
   // ---- one partial slab per block: each wave writes its own rows
-  const size_t slab = (size_t)blockIdx.x * a.Mtot;
+  const size_t slab = (size_t)(blockIdx.x + a.kb0) * a.Mtot;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
 #pragma unroll
@@ -505,8 +506,9 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     }
   };
 
-  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t_beg = blockIdx.x * tpb_;
+  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int tpb_ = (total + KBt - 1) / KBt;
+  const int t_beg = kbi * tpb_;
   const int t_end = min(total, t_beg + tpb_);
   if (t_beg < t_end) load(t_beg);
   for (int tt = t_beg; tt < t_end; ++tt) {
@@ -542,7 +544,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     }
   }
 
-  const size_t slab = (size_t)blockIdx.x * a.Mtot;
+  const size_t slab = (size_t)(blockIdx.x + a.kb0) * a.Mtot;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
 #pragma unroll

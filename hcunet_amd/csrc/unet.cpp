@@ -1136,7 +1136,8 @@ void decide_ap(Ctx &c, const ConvLayer &L, bool with_dgrad) {
 // BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
-                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
+                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr,
+                  bool split_last = false) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
   const bool ap = c.ap(L);
@@ -1153,7 +1154,22 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
     w.g_c0 = lc.c0;
   }
   if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
-  if (int e = launch_wgrad(w, c.wstream())) return e;
+  // The last layer's weight gradient (no input gradient follows): the chain
+  // has nothing left to do but wait for the branch, so half of the voxel
+  // blocks run on each stream (disjoint slabs, the same finalize and bits).
+  static const bool split_on = !(getenv("HCU_SPLIT_LAST") && getenv("HCU_SPLIT_LAST")[0] == '0');
+  if (split_last && split_on && c.split && !dA && (w.v2 != 0 || w.use_bw) && w.KB >= 2) {
+    WGradArgs w1 = w, w2 = w;
+    w1.kbn = w2.kbn = w.KB;
+    w1.kb0 = 0;
+    w1.KB = w.KB / 2;
+    w2.kb0 = w1.KB;
+    w2.KB = w.KB - w1.KB;
+    if (int e = launch_wgrad(w2, c.wstream())) return e;
+    if (int e = launch_wgrad(w1, c.s)) return e;
+  } else if (int e = launch_wgrad(w, c.wstream())) {
+    return e;
+  }
   WGradFinalize f{};
   f.partial = w.partial;
   f.dw = c.G + L.w_off;
@@ -1743,7 +1759,8 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.alloc(sa)) return e;
       dIn = c.buf(sa);
     }
-    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training))
+    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training,
+                              nullptr, i == 0))
       return e;
     if (i > 0) {
       // dIn = d(pooled): produce d(pre-BN y2_{i-1}) into a fresh slot
@@ -1763,6 +1780,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = grads_ready(p.grad_ev[1])) return e;
   }
   tag(std::string("wgrad"), "finalize");
+  if (int e = c.fork()) return e;   // (the last weight gradient may have run half on the chain)
   if (int e = c.flush_wgf()) return e;
   if (int e = c.join()) return e;
   if (timing_on()) timing_set_tag("");

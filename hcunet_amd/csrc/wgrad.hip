@@ -322,9 +322,10 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
   const int HAV = a.HAX * a.HAY * a.HAZ;        // real halo extent
   const int PTr = a.TX * a.TY * a.TZ;           // real tile extent
 
-  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t_end = min(total, (int)blockIdx.x * tpb_ + tpb_);
-  for (int tt = blockIdx.x * tpb_; tt < t_end; ++tt) {
+  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int tpb_ = (total + KBt - 1) / KBt;
+  const int t_end = min(total, kbi * tpb_ + tpb_);
+  for (int tt = kbi * tpb_; tt < t_end; ++tt) {
     const int b = tt / ntiles;
     int tile = tt - b * ntiles;
     const int tzi = tile % a.ntz;
@@ -466,7 +467,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
     }
     lds_barrier();
   }
-  const int kb = blockIdx.x;
+  const int kb = kbi;
   const int nel = MS * NS * 256;
   for (int idx = tid; idx < nel; idx += 256) {
     const int r = idx & 3, ln = (idx >> 2) & 63, ti = idx >> 8;

@@ -122,8 +122,9 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   const int nzq = a.ntz > 1 ? 5 : 4;                 // z quad -1 (slot 3) only when z tiles have a predecessor
   const int nG = CG4 * NXY * nzq;
   const FastDiv fTY = a.fTY;
-  const int tpb = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t_beg = (int)blockIdx.x * tpb;
+  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int tpb = (total + KBt - 1) / KBt;
+  const int t_beg = kbi * tpb;
   const int t_end = min(total, t_beg + tpb);
 
   // staging cells of this thread (at most 2 A and 2 G cells: plan_wgrad8)
@@ -337,7 +338,7 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   for (int i = 0; i < NACC; ++i)
     *reinterpret_cast<floatx4 *>(red + ((wave * NR + i) * 64 + lane) * 4) = acc[i];
   lds_barrier();
-  const int kb = blockIdx.x;
+  const int kb = kbi;
   const int T = KXY * a.KZ;
   if constexpr (MODE == 0) {
     for (int idx = tid; idx < NR * 256; idx += 256) {

@@ -12,6 +12,31 @@
 #define HCU_BCONV_PHASES 1
 #include "../hcunet_amd/csrc/bconv.hip"
 #include "../hcunet_amd/csrc/bconv_f32.hip"
+// The instances of one channel-group width only (BENCH_CV = 1, 2 or 4; the
+// others report "unsupported variant"): one per-CV translation unit each.
+#ifndef BENCH_CV
+#define BENCH_CV 4
+#endif
+#define BENCH_STUB(E_, CV_)                                                                         \
+  namespace hcu {                                                                                  \
+  template <>                                                                                      \
+  bool bconv_launch_cv<E_, CV_>(const GConvArgs &, hipStream_t, const dim3 &, double, double) {    \
+    return false;                                                                                  \
+  }                                                                                                \
+  }
+#if BENCH_CV == 1
+#include "../hcunet_amd/csrc/bconv_f32_cv1.hip"
+#include "../hcunet_amd/csrc/bconv_bf16_cv1.hip"
+BENCH_STUB(float, 2) BENCH_STUB(float, 4) BENCH_STUB(uint16_t, 2) BENCH_STUB(uint16_t, 4)
+#elif BENCH_CV == 2
+#include "../hcunet_amd/csrc/bconv_f32_cv2.hip"
+#include "../hcunet_amd/csrc/bconv_bf16_cv2.hip"
+BENCH_STUB(float, 1) BENCH_STUB(float, 4) BENCH_STUB(uint16_t, 1) BENCH_STUB(uint16_t, 4)
+#else
+#include "../hcunet_amd/csrc/bconv_f32_cv4.hip"
+#include "../hcunet_amd/csrc/bconv_bf16_cv4.hip"
+BENCH_STUB(float, 1) BENCH_STUB(float, 2) BENCH_STUB(uint16_t, 1) BENCH_STUB(uint16_t, 2)
+#endif
 
 #include <chrono>
 #include <cstring>

@@ -3,6 +3,7 @@
 # compiled in with HCU_BCONV_PHASES).
 set -euo pipefail
 cd "$(dirname "$0")/.."
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ihcunet_amd/csrc \
-  tools/bconv_bench.hip hcunet_amd/csrc/timing.cpp -o tools/bconv_bench
-echo "built tools/bconv_bench"
+CV=${1:-4}
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ihcunet_amd/csrc -DBENCH_CV=$CV \
+  tools/bconv_bench.hip hcunet_amd/csrc/timing.cpp -o tools/bconv_bench_cv$CV
+echo "built tools/bconv_bench_cv$CV"
