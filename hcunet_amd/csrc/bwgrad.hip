@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
   const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
 
   // contiguous tile range per block (consecutive tiles share halo rows in L2)
-  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int KBt = (int)gridDim.x, kbi = (int)blockIdx.x;
   const int tpb_ = (total + KBt - 1) / KBt;
   const int t_end = min(total, kbi * tpb_ + tpb_);
   for (int tt = kbi * tpb_; tt < t_end; ++tt) {
@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
   }
 
   // ---- one partial slab per block: each wave writes its own rows
-  const size_t slab = (size_t)(blockIdx.x + a.kb0) * a.Mtot;
+  const size_t slab = (size_t)blockIdx.x * a.Mtot;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
 #pragma unroll
@@ -506,7 +506,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     }
   };
 
-  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int KBt = (int)gridDim.x, kbi = (int)blockIdx.x;
   const int tpb_ = (total + KBt - 1) / KBt;
   const int t_beg = kbi * tpb_;
   const int t_end = min(total, t_beg + tpb_);
@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     }
   }
 
-  const size_t slab = (size_t)(blockIdx.x + a.kb0) * a.Mtot;
+  const size_t slab = (size_t)blockIdx.x * a.Mtot;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
 #pragma unroll

@@ -598,10 +598,6 @@ struct WGradArgs {
   // stride phases are extra output columns and the bias row sums dU per
   // (q, co) -- no separate chansum.  nph <= 1: plain Conv3d form.
   int nph, phx, phy, phz, GCout;
-  // A launch covering slabs kb0 .. kb0 + KB - 1 of a weight gradient split
-  // into kbn voxel blocks (kbn == 0: the whole gradient, kb0 = 0): the last
-  // layer's weight gradient runs half on each stream (Ctx, split_last).
-  int kb0, kbn;
 };
 int plan_bwgrad(WGradArgs &a, int target_blocks);
 int launch_bwgrad(const WGradArgs &a, hipStream_t s);

@@ -249,10 +249,11 @@ int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, i
     const char *e = getenv("HCU_PREP_PERM");
     return !(e && e[0] == '0');
   }();
-  // HCU_PREP_TILED=0: every job on the gather form (A/B)
+  // HCU_PREP_TILED=1 (opt-in): the LDS-staged form where it applies; measured
+  // 22 -> 33 us per config-2 step and equal on config 3, so the gather stays
   static const bool tiled = [] {
     const char *e = getenv("HCU_PREP_TILED");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   for (int j0 = 0; j0 < n; j0 += kPrepBatch) {
     PrepBatch b{};

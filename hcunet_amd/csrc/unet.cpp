@@ -433,7 +433,9 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     max_part = std::max(max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
   }
   u.wg_phase = false;
-  static const bool phase_on = !(getenv("HCU_CONVT_PHASE_WG") && getenv("HCU_CONVT_PHASE_WG")[0] == '0');
+  // opt-in (HCU_CONVT_PHASE_WG=1): measured +13 us per config-2 step against the
+  // per-tap wgrad_kernel + chansum (its wider slabs double the finalize reads)
+  static const bool phase_on = getenv("HCU_CONVT_PHASE_WG") && getenv("HCU_CONVT_PHASE_WG")[0] == '1';
   if (!bf && u.fused && o % 4 == 0 && phase_on) {
     // dW'[(j, ci)][(q, co)] = sum_o A[o + j - (J-1)][ci] * dU[o*S + q][co] over the
     // phase grid o (the forward's fused GEMM, hcat/unet.py:294-298)
@@ -981,10 +983,12 @@ void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
 }
 
-// HCU_BNB_TAIL=0: the separate bn_bwd_finalize launch for every BatchNorm
-// backward instead of the last-workgroup finalize (BnbFin; A/B)
+// HCU_BNB_TAIL=1 (opt-in): the BatchNorm-backward finalize in the producing
+// dgrad's last workgroup (BnbFin) instead of the bn_bwd_finalize launch;
+// measured +10 us per config-2 step (the last workgroup's serial reduction
+// costs more than the launch it removes)
 bool tails_enabled() {
-  static const bool on = !(getenv("HCU_BNB_TAIL") && getenv("HCU_BNB_TAIL")[0] == '0');
+  static const bool on = getenv("HCU_BNB_TAIL") && getenv("HCU_BNB_TAIL")[0] == '1';
   return on;
 }
 
@@ -1103,25 +1107,26 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 // input gradient -- can apply the BatchNorm backward on load (dz*scale +
 // c1*y + c0 while staging the operand), so dY(L) is never materialised: the
 // input gradient on bconv (AP instances), the weight gradient on wgrad2,
-// wgrad8 form 0 or the pipelined bwgrad.  HCU_AP=0 materialises every dY
-// (the bn_bwd_apply pass, A/B); HCU_AP_BF16=0 only the bf16 ones.
+// wgrad8 form 0 or the pipelined bwgrad.
+// Default: only the fp32 first layer's weight gradient (wgrad8 form 0, no
+// input gradient: round 3, the 31 us apply pass gone from the chain's end).
+// HCU_AP=1 extends it to every layer that qualifies (opt-in: measured
+// +27 us per config-2 step, -20 us on config 3 in one run -- a consumer
+// staging dz and y runs 15-40 % longer, which costs what the apply pass and
+// its launch save); HCU_AP=0 materialises every dY (A/B).
 bool ap_ok(const Ctx &c, const ConvLayer &L, bool with_dgrad) {
-  static const bool on = !(getenv("HCU_AP") && getenv("HCU_AP")[0] == '0');
+  static const int mode = getenv("HCU_AP") ? atoi(getenv("HCU_AP")) : -1;
   static const bool bf_on = !(getenv("HCU_AP_BF16") && getenv("HCU_AP_BF16")[0] == '0');
-  // Measured on MI355X (config 2): a consumer staging dz and y runs 15-40 %
-  // longer on a large layer (d1/d2: two HBM operand streams), which costs more
-  // than the apply pass it removes; on the small deep layers the launch saved
-  // dominates.  HCU_AP_MAX_MB: the largest dY (MB) applied on load.
+  // HCU_AP_MAX_MB: the largest dY (MB) applied on load.
   static const double max_b = 1e6 * (getenv("HCU_AP_MAX_MB") ? atof(getenv("HCU_AP_MAX_MB")) : 8.0);
-  if (!on || c.p.is_chain || L.bn.index >= 64) return false;
+  if (mode == 0 || c.p.is_chain || L.bn.index >= 64) return false;
+  const WGradArgs &w = L.wg;
+  if (mode < 0) return !with_dgrad && w.v2 == 2 && w.w8mode == 0 && w.GCs <= 16;
   const bool small = (double)L.out.vox() * L.out.Cs * L.out.es <= max_b;
   if (with_dgrad && (!small || !L.dgrad.use_bconv)) return false;
-  const WGradArgs &w = L.wg;
   // (the bf16 first layer's bwgrad with the operand apply ran 253 us against
   // 115 + 116 for bwgrad + the apply pass: only small bf16 layers)
   if (w.use_bw) return bf_on && small && bwgrad_gap_ok(w);
-  // wgrad8 form 0: the fp32 first layer (no input gradient) applies on load
-  // at any size (round 3: the 31 us apply pass gone from the chain's end)
   if (w.v2 == 2) return w.w8mode == 0 && w.GCs <= 16 && (small || !with_dgrad);
   return w.v2 == 1 && small;
 }
@@ -1136,8 +1141,7 @@ void decide_ap(Ctx &c, const ConvLayer &L, bool with_dgrad) {
 // BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
-                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr,
-                  bool split_last = false) {
+                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
   const bool ap = c.ap(L);
@@ -1154,22 +1158,7 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
     w.g_c0 = lc.c0;
   }
   if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
-  // The last layer's weight gradient (no input gradient follows): the chain
-  // has nothing left to do but wait for the branch, so half of the voxel
-  // blocks run on each stream (disjoint slabs, the same finalize and bits).
-  static const bool split_on = !(getenv("HCU_SPLIT_LAST") && getenv("HCU_SPLIT_LAST")[0] == '0');
-  if (split_last && split_on && c.split && !dA && (w.v2 != 0 || w.use_bw) && w.KB >= 2) {
-    WGradArgs w1 = w, w2 = w;
-    w1.kbn = w2.kbn = w.KB;
-    w1.kb0 = 0;
-    w1.KB = w.KB / 2;
-    w2.kb0 = w1.KB;
-    w2.KB = w.KB - w1.KB;
-    if (int e = launch_wgrad(w2, c.wstream())) return e;
-    if (int e = launch_wgrad(w1, c.s)) return e;
-  } else if (int e = launch_wgrad(w, c.wstream())) {
-    return e;
-  }
+  if (int e = launch_wgrad(w, c.wstream())) return e;
   WGradFinalize f{};
   f.partial = w.partial;
   f.dw = c.G + L.w_off;
@@ -1759,8 +1748,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       if (int e = c.alloc(sa)) return e;
       dIn = c.buf(sa);
     }
-    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training,
-                              nullptr, i == 0))
+    if (int e = conv_backward(c, c1, in, nullptr, nullptr, Bf, sb, dIn, accumulate, nullptr, training))
       return e;
     if (i > 0) {
       // dIn = d(pooled): produce d(pre-BN y2_{i-1}) into a fresh slot

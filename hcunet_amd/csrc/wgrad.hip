@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
   const int HAV = a.HAX * a.HAY * a.HAZ;        // real halo extent
   const int PTr = a.TX * a.TY * a.TZ;           // real tile extent
 
-  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int KBt = (int)gridDim.x, kbi = (int)blockIdx.x;
   const int tpb_ = (total + KBt - 1) / KBt;
   const int t_end = min(total, kbi * tpb_ + tpb_);
   for (int tt = kbi * tpb_; tt < t_end; ++tt) {

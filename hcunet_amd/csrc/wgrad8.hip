@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   const int nzq = a.ntz > 1 ? 5 : 4;                 // z quad -1 (slot 3) only when z tiles have a predecessor
   const int nG = CG4 * NXY * nzq;
   const FastDiv fTY = a.fTY;
-  const int KBt = a.kbn ? a.kbn : (int)gridDim.x, kbi = (int)blockIdx.x + a.kb0;   // (WGradArgs::kb0)
+  const int KBt = (int)gridDim.x, kbi = (int)blockIdx.x;
   const int tpb = (total + KBt - 1) / KBt;
   const int t_beg = kbi * tpb;
   const int t_end = min(total, t_beg + tpb);

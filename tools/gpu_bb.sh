@@ -22,4 +22,10 @@ run 4 4 f 2 124 124 14 16 16 3 3 1 1     # d1.c2 fwd
 run 4 4 f 2 59 59 13 32 32 3 3 1 1       # d2.c2 fwd
 run 4 4 f 2 28 28 13 32 64 3 3 2 0       # d3.c1 fwd
 run 4 4 f 2 12 12 12 64 128 3 3 2 0      # d4.c1 fwd
-cat $O/${TAG}.txt
+
+# variants of config 3 d0.c2 fwd: direct staging (no register prefetch), fewer subtiles
+HCU_BCONV_FORCE=32,2,4,0 run 4 2 f 4 254 254 15 32 32 3 3 1 1
+HCU_BCONV_FORCE=32,2,2 run 4 2 f 4 254 254 15 32 32 3 3 1 1
+HCU_BCONV_FORCE=32,1,4 run 4 2 f 4 254 254 15 32 32 3 3 1 1
+HCU_BCONV_LDS_KB=160 HCU_BCONV_FORCE=32,2,4 run 4 2 f 4 254 254 15 32 32 3 3 1 1
+tail -12 $O/${TAG}.txt
