@@ -33,9 +33,10 @@ from hcat.loss import cross_entropy  # noqa: E402
 from hcat.unet import Unet_Constructor  # noqa: E402
 import hcunet_amd  # noqa: E402
 from hcunet_amd import _lib  # noqa: E402
+import hcunet_amd.chain  # noqa: E402
 from hcunet_amd import roofline as roofline_mod  # noqa: E402
 
-PROFILE_TAG = 'r03'   # the round whose committed profiles/ summaries bench.py cites
+PROFILE_TAG = 'r04'   # the round whose committed profiles/ summaries bench.py cites
 
 METRIC = "training voxels/sec (fwd+bwd+step), 5-level 3D U-Net, 256×256×16×4 tiles"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, dense
@@ -210,7 +211,9 @@ def rocprof_avg_us(kernel, config, kind=''):
     chain); 'serial_' the same bench with HCU_SIDE=0, one kernel at a time --
     the conditions of the HIP-event timing pass."""
     import csv
-    path = os.path.join(ROOT, 'profiles', '%s_kernel_stats_%sconfig%s.csv' % (PROFILE_TAG, kind, config))
+    name = ('%s_kernel_stats_%s.csv' % (PROFILE_TAG, config) if config == 'runet'
+            else '%s_kernel_stats_%sconfig%s.csv' % (PROFILE_TAG, kind, config))
+    path = os.path.join(ROOT, 'profiles', name)
     try:
         with open(path, newline='') as f:
             rows = list(csv.DictReader(f))
@@ -355,13 +358,36 @@ def runet_main(args):
     el = (time.perf_counter() - t0) / args.steps
     vox = RUNET_TILE[0] * RUNET_TILE[1] * RUNET_TILE[2]
     roofline = kernels = None
+    layers = None
     if not args.no_kernel_timing:
         _lib.lib().hcu_timing_enable(args.steps * 2048)
+        _lib.lib().hcu_timing_detail(1)
+        hcunet_amd.chain.TAG_CHAINS = True
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize(device)
-        rep = _lib.timing_report()
+        hcunet_amd.chain.TAG_CHAINS = False
+        detail = _lib.timing_report()
+        _lib.lib().hcu_timing_detail(0)
         _lib.lib().hcu_timing_disable()
+        rep = {}
+        per_layer = {}
+        for k, v in detail.items():   # per kernel symbol, and per chain op tag
+            r = rep.setdefault(k.partition('@')[0], dict(count=0, ms=0.0, flops=0.0, bytes=0.0))
+            for f in r:
+                r[f] += v[f]
+            layer, phase = layer_of(k)
+            lr = per_layer.setdefault(layer, dict(layer=layer, us=0.0, launches=0.0, gflop=0.0, kernels={}))
+            lr['us'] += v['ms'] * 1e3 / args.steps
+            lr['launches'] += v['count'] / args.steps
+            lr['gflop'] += v['flops'] / args.steps / 1e9
+            kk = '%s:%s' % (phase, k.partition('@')[0])
+            lr['kernels'][kk] = round(lr['kernels'].get(kk, 0.0) + v['ms'] * 1e3 / args.steps, 2)
+        layers = sorted(({"layer": r['layer'], "measured_us": round(r['us'], 2), "launches": r['launches'],
+                          "gflop": round(r['gflop'], 4),
+                          "tflops": round(r['gflop'] / r['us'] * 1e-3, 2) if r['us'] else None,
+                          "kernels": r['kernels']} for r in per_layer.values()),
+                        key=lambda r: -r['measured_us'])
         total_ms = sum(v['ms'] for v in rep.values())
         name, d = max(rep.items(), key=lambda kv: kv[1]['ms'])
         avg_s = d['ms'] / d['count'] / 1e3
@@ -371,10 +397,16 @@ def runet_main(args):
             peak = PEAK_BF16_MFMA_TFLOPS if bf_kernel else PEAK_FP32_MFMA_TFLOPS
         else:
             ach, bound, unit, peak = d['bytes'] / d['count'] / avg_s / 1e9, 'hbm', 'GB/s', PEAK_HBM_GBS
+        rp_us = rocprof_avg_us(name, 'runet')
         roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
                     "traffic": None, "kernel": name, "avg_launch_us": avg_s * 1e6,
+                    "flops_per_launch": d['flops'] / d['count'] if d['flops'] > 0 else None,
+                    "bytes_per_launch": d['bytes'] / d['count'] if d['bytes'] > 0 else None,
+                    "rocprof_avg_launch_us": rp_us,
+                    "rocprof_summary": 'profiles/%s_kernel_stats_runet.csv' % PROFILE_TAG if rp_us else None,
                     "launches_per_step": d['count'] / args.steps, "share_of_kernel_time": d['ms'] / total_ms}
         kernels = {"kernel_ms_per_step": total_ms / args.steps,
+                   "launches_per_step": sum(v['count'] for v in rep.values()) / args.steps,
                    "algorithmic_tflops_per_step": sum(v['flops'] for v in rep.values()) / args.steps / 1e12,
                    "top": sorted(({"kernel": k, "ms_per_step": v['ms'] / args.steps,
                                    "launches_per_step": v['count'] / args.steps} for k, v in rep.items()),
@@ -407,7 +439,7 @@ def runet_main(args):
                                    "stacked dilations 1..5), B=1, 512x512x24x4 tiles from pinned host "
                                    "memory with async prefetch, bf16 autocast",
                        "final_loss": float(loss.item())},
-            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels}
+            "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "layers": layers}
     print(json.dumps(line), flush=True)
 
 

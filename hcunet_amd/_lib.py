@@ -122,6 +122,7 @@ SYMBOLS = [
     ("hcu_timing_enable", _I, [_I]),
     ("hcu_timing_disable", _I, []),
     ("hcu_timing_detail", _I, [_I]),
+    ("hcu_timing_prefix", _I, [ctypes.c_char_p]),
     ("hcu_timing_report", _I64, [ctypes.c_char_p, _I64]),
     ("hcu_chain_plan_create", _I, [_VP, _I, _I, _I, _I, ctypes.POINTER(_VP)]),
     ("hcu_chain_plan_query", _I, [_VP, ctypes.POINTER(_I64), ctypes.POINTER(_I), ctypes.POINTER(_SZ),

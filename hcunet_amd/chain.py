@@ -24,6 +24,9 @@ from . import _lib
 
 CONV, POOL, CONVT = 0, 1, 2
 MAX_OPS = 16
+# bench.py's per-layer timing pass: each chain call tags its launches with the
+# chain's name (hcu_timing_prefix) so the report tells the chains apart
+TAG_CHAINS = False
 
 
 class ChainOp(ctypes.Structure):
@@ -151,9 +154,10 @@ class Chain:
     ('conv', nn.Conv3d, bn or None, cat_fold) / ('pool', kernel) /
     ('convt', nn.ConvTranspose3d)."""
 
-    def __init__(self, flat, in_channels, ops):
+    def __init__(self, flat, in_channels, ops, name=''):
         if not 1 <= len(ops) <= MAX_OPS:
             raise ValueError('a chain has 1..%d ops' % MAX_OPS)
+        self.name = name
         self.flat = flat
         self.in_channels = in_channels
         self.ops = ops
@@ -311,9 +315,14 @@ class _ChainFunction(torch.autograd.Function):
         saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
         t = _tensors(chain, x, out, saved, scratch)
+        L = _lib.lib()
+        if TAG_CHAINS:
+            L.hcu_timing_prefix(chain.name.encode())
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().hcu_chain_forward(plan.handle, ctypes.byref(t), 1 if training else 0,
-                                                    _lib.stream_handle(dev)), 'chain forward')
+            _lib.check(L.hcu_chain_forward(plan.handle, ctypes.byref(t), 1 if training else 0,
+                                           _lib.stream_handle(dev)), 'chain forward')
+        if TAG_CHAINS:
+            L.hcu_timing_prefix(b'')
         ctx.chain, ctx.plan, ctx.training = chain, plan, training
         ctx.save_for_backward(x, saved)
         return out
@@ -329,11 +338,16 @@ class _ChainFunction(torch.autograd.Function):
         dx = torch.empty(x.shape, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
         G, finish = chain.flat.grad_target()
         t = _tensors(chain, x, None, saved, scratch, grads=G)
+        L = _lib.lib()
+        if TAG_CHAINS:
+            L.hcu_timing_prefix(chain.name.encode())
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().hcu_chain_backward(plan.handle, ctypes.byref(t),
-                                                     ctypes.c_void_p(dout.data_ptr()), _lib.ptr(dx),
-                                                     1 if ctx.training else 0, 1, _lib.stream_handle(dev)),
+            _lib.check(L.hcu_chain_backward(plan.handle, ctypes.byref(t),
+                                            ctypes.c_void_p(dout.data_ptr()), _lib.ptr(dx),
+                                            1 if ctx.training else 0, 1, _lib.stream_handle(dev)),
                        'chain backward')
+        if TAG_CHAINS:
+            L.hcu_timing_prefix(b'')
         finish()
         if dx is not None and dx.dtype != x.dtype:
             dx = dx.to(x.dtype)

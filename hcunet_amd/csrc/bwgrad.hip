@@ -587,6 +587,18 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// CUs' worth of resident workgroups the bf16 weight gradient is sized for
+// (HCU_BW_CUS, A/B): fewer voxel blocks write fewer fp32 slabs for the
+// finalize to read, and leave the chain's kernels room on the CUs.
+static int bw_cus() {
+  static const int v = [] {
+    const char *e = getenv("HCU_BW_CUS");
+    const int n = e ? atoi(e) : 256;
+    return n < 16 ? 16 : (n > 256 ? 256 : n);
+  }();
+  return v;
+}
+
 int plan_bwgrad(WGradArgs &a, int target_blocks) {
   a.use_bw = 0;
   const int T = a.KX * a.KY * a.KZ;
@@ -684,7 +696,7 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   // blocks, fewer slabs for the finalize to read.
   const int occ_cap = getenv("HCU_BW_OCC") ? std::max(1, atoi(getenv("HCU_BW_OCC"))) : 2;
   const int occ_kb = a.NPA ? std::min(a.occ, occ_cap) : a.occ;
-  long kb = std::max(1L, (long)256 * occ_kb / per);
+  long kb = std::max(1L, (long)bw_cus() * occ_kb / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
   a.use_bw = 1;

@@ -85,6 +85,18 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
 
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// CUs' worth of resident workgroups a weight-gradient launch (the backward's
+// branch stream) is sized for: 256 fills the chip; fewer leave slots for the
+// chain stream's kernels to start while the branch runs (HCU_SIDE_CUS, A/B).
+inline int side_cus() {
+  static const int v = [] {
+    const char *e = getenv("HCU_SIDE_CUS");
+    const int n = e ? atoi(e) : 256;
+    return n < 16 ? 16 : (n > 256 ? 256 : n);
+  }();
+  return v;
+}
 inline size_t align_up(size_t a, size_t b) { return (a + b - 1) / b * b; }
 
 // Division by a runtime-constant divisor without the ~40-instruction integer

@@ -23,6 +23,7 @@ std::mutex g_mu;
 bool g_on = false;
 bool g_detail = false;
 thread_local std::string g_tag;
+thread_local std::string g_prefix;   // hcu_timing_prefix: the calling chain's name
 std::vector<hipEvent_t> g_pool;
 std::vector<Rec> g_recs;
 size_t g_next = 0;
@@ -31,7 +32,7 @@ size_t g_next = 0;
 bool timing_on() { return g_on; }
 
 void timing_set_tag(const char *tag) {
-  if (g_on) g_tag = tag ? tag : "";
+  if (g_on) g_tag = (g_prefix.empty() ? std::string() : g_prefix + ":") + (tag ? tag : "");
 }
 
 int timing_begin(hipStream_t s, const std::string &name, double flops, double bytes) {
@@ -70,6 +71,11 @@ int hcu_timing_enable(int max_launches) {
 int hcu_timing_detail(int on) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_detail = on != 0;
+  return HCU_OK;
+}
+
+int hcu_timing_prefix(const char *prefix) {
+  g_prefix = prefix ? prefix : "";
   return HCU_OK;
 }
 

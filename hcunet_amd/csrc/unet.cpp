@@ -1107,21 +1107,18 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 // input gradient -- can apply the BatchNorm backward on load (dz*scale +
 // c1*y + c0 while staging the operand), so dY(L) is never materialised: the
 // input gradient on bconv (AP instances), the weight gradient on wgrad2,
-// wgrad8 form 0 or the pipelined bwgrad.
-// Default: only the fp32 first layer's weight gradient (wgrad8 form 0, no
-// input gradient: round 3, the 31 us apply pass gone from the chain's end).
-// HCU_AP=1 extends it to every layer that qualifies (opt-in: measured
-// +27 us per config-2 step, -20 us on config 3 in one run -- a consumer
-// staging dz and y runs 15-40 % longer, which costs what the apply pass and
-// its launch save); HCU_AP=0 materialises every dY (A/B).
+// wgrad8 form 0 or the pipelined bwgrad.  Opt-in (HCU_AP=1): measured on
+// MI355X, every qualifying layer +27 us per config-2 step (-20 us on config 3
+// in one run) -- a consumer staging dz and y runs 15-40 % longer, which costs
+// what the apply pass and its launch save -- and the first layer's weight
+// gradient alone (the round-3 default) +7 us per config-2 step.
 bool ap_ok(const Ctx &c, const ConvLayer &L, bool with_dgrad) {
-  static const int mode = getenv("HCU_AP") ? atoi(getenv("HCU_AP")) : -1;
+  static const int mode = getenv("HCU_AP") ? atoi(getenv("HCU_AP")) : 0;
   static const bool bf_on = !(getenv("HCU_AP_BF16") && getenv("HCU_AP_BF16")[0] == '0');
   // HCU_AP_MAX_MB: the largest dY (MB) applied on load.
   static const double max_b = 1e6 * (getenv("HCU_AP_MAX_MB") ? atof(getenv("HCU_AP_MAX_MB")) : 8.0);
   if (mode == 0 || c.p.is_chain || L.bn.index >= 64) return false;
   const WGradArgs &w = L.wg;
-  if (mode < 0) return !with_dgrad && w.v2 == 2 && w.w8mode == 0 && w.GCs <= 16;
   const bool small = (double)L.out.vox() * L.out.Cs * L.out.es <= max_b;
   if (with_dgrad && (!small || !L.dgrad.use_bconv)) return false;
   // (the bf16 first layer's bwgrad with the operand apply ran 253 us against

@@ -547,7 +547,7 @@ static int plan_wgrad2(WGradArgs &a, int target_blocks) {
   const long total = (long)a.B * a.ntx * a.nty * a.ntz;
   const long per = (long)a.mchunks * a.nchunks;
   a.occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
-  long kb = std::max(1L, (long)256 * a.occ / per);
+  long kb = std::max(1L, (long)side_cus() * a.occ / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
   a.v2 = 1;
@@ -656,7 +656,7 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   a.ntz = ntz;
   const long total = (long)a.B * a.ntx * a.nty * a.ntz;
   const long per = (long)a.mchunks * a.nchunks;
-  long kb = std::max(1L, (long)target_blocks / per);
+  long kb = std::max(1L, (long)target_blocks * side_cus() / 256 / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
   if (a.nph > 1) {   // the phase form runs on wgrad2 only

@@ -556,7 +556,7 @@ int plan_wgrad8(WGradArgs &a) {
   const long total = (long)a.B * a.ntx * a.nty * a.ntz;
   long best_kb = 1, best_cost = 1L << 62;
   for (int per_cu = 1; per_cu <= 2; ++per_cu) {
-    const long kb = std::min(total, (long)256 * per_cu / nci);
+    const long kb = std::min(total, (long)side_cus() * per_cu / nci);
     if (kb < 1) continue;
     const long cost = cdiv(total, kb) * per_cu;
     if (cost < best_cost || (cost == best_cost && kb > best_kb)) {

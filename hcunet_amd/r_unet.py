@@ -48,7 +48,7 @@ def _chain(owner, root, name, in_channels, ops):
     key = (id(root), name)
     ch = cache.get(key)
     if ch is None or ch.flat.root is not root:
-        ch = Chain(flat_of(root), in_channels, ops)
+        ch = Chain(flat_of(root), in_channels, ops, '%s.%s' % (type(owner).__name__, name))
         cache[key] = ch
     return ch
 

@@ -398,6 +398,9 @@ int hcu_timing_enable(int max_launches);
 int hcu_timing_disable(void);
 /* on != 0: report per network layer ("kernel@layer") instead of per symbol. */
 int hcu_timing_detail(int on);
+/* Prefix of this thread's launch tags in the detail records (a chain's name,
+ * hcunet_amd/chain.py); empty or null: none. */
+int hcu_timing_prefix(const char *prefix);
 /* One line per kernel symbol: name\tcount\ttotal_ms\tflops\tbytes (totals
  * over launches; flops/bytes are algorithmic).  Returns bytes needed. */
 int64_t hcu_timing_report(char *buf, int64_t len);

@@ -169,8 +169,9 @@ def test_opt_in_fusions_match_default(tmp_path, bf16):
     (HCU_PREP_TILED=1).  Together they give the default's outputs and
     gradients to fp32 re-association (the coefficients and slab sums are
     reassociated: 1e-4 of each tensor's largest element; bf16: 2e-2, one bf16
-    rounding of a reassociated operand), and two runs of them are bitwise
-    equal."""
+    rounding of a reassociated operand; plus an absolute 1e-6 for the biases
+    ahead of a BatchNorm, whose gradients are rounding noise about 0), and two
+    runs of them are bitwise equal."""
     kw = KW if bf16 == '0' else KW.replace('[8, 16, 32, 64, 128]', '[16, 32, 64, 128]')
     ref = _run(tmp_path, 'def' + bf16, {'HCU_TEST_BF16': bf16}, kw=kw)
     on = _run(tmp_path, 'opt' + bf16, dict(OPT_IN, HCU_TEST_BF16=bf16), kw=kw)
@@ -179,7 +180,7 @@ def test_opt_in_fusions_match_default(tmp_path, bf16):
     for it in range(3):
         for k, (a, b, c) in enumerate(zip(ref[it], on[it], on2[it])):
             assert torch.equal(b, c), (it, k)
-            tol = rel * max(a.abs().max().item(), 1e-6)
+            tol = rel * a.abs().max().item() + 1e-6
             assert (a - b).abs().max().item() <= tol, (it, k, (a - b).abs().max().item(), tol)
 
 

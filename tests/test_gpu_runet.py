@@ -216,3 +216,61 @@ def test_rdcnet_bf16_autocast_relative():
     assert ours['out'] <= 1.5 * auto['out'] + 1e-3
     assert ours['g'] <= 1.5 * auto['g'] + 1e-2
     assert abs(loss.item() - ref_loss) <= 1e-2 * abs(ref_loss)
+
+
+def test_rdcnet_full_tile_512x512x24_matches_oracle():
+    """BASELINE config 5's tile: RDCNet(4, 5) fp32 train step (forward, pixel
+    BCE + MSE, backward) on one 512x512x24 tile, where the dilated 5^3
+    convolutions run their sub-lattice (space-to-batch) tilings that the small
+    fixture never picks.  Checked against the oracle restatement
+    (oracle/runet_oracle.py, pinned to the reference by runet_rdc.npz) run on
+    the host in fp32 (an fp64 oracle step takes ~15 min of host time here:
+    torch's CPU fp64 dilated convolution has no fast path; the fixture test
+    carries the fp64-anchored bar).  Bars, for two fp32 computations in
+    different summation orders: output within 2e-4 of its largest element,
+    loss within 1e-5 relative, every gradient within 1e-3 relative L2 and 1e-3
+    of its largest element (measured: see the printed report)."""
+    from oracle import loss_oracle as lo
+    from oracle import runet_oracle as ro
+    torch.set_num_threads(16)
+    torch.manual_seed(7)
+    net = RDCNet(4, 5)
+    st = ro.state_of(net, torch.float32)
+    shape = (1, 4, 512, 512, 24)
+    x = inputs.make_x(shape)
+    oshape = (1, 5) + shape[2:]
+    mshape = (1, 1) + shape[2:]
+    mask, pwl = inputs.make_mask(mshape), inputs.make_pwl(mshape)
+    vec = (inputs.make_x((1, 3) + shape[2:], seed=4) * 0.5).astype(np.float32)
+    g = {'out_shape': oshape, 'vec': vec}
+    net = net.cuda().train()
+    out, loss = _train_step_with(net, g, x, mask, pwl)
+    o = ro.rdcnet_forward(st, torch.from_numpy(x))
+    ls = lo.cross_entropy(o[:, 0:1], torch.from_numpy(mask).float(), torch.from_numpy(pwl),
+                          method='pixel') + lo.MSELoss(o[:, 2:], torch.from_numpy(vec))
+    ls.backward()
+    o = o.detach()
+    rows = []
+    err = (out - o).abs().max().item()
+    bar = 2e-4 * o.abs().max().item() + 1e-6
+    rows.append((err <= bar, 'out: max err %.3g, bar %.3g' % (err, bar)))
+    lerr = abs(loss - ls.item()) / abs(ls.item())
+    rows.append((lerr <= 1e-5, 'loss: rel err %.3g (%.6f vs %.6f)' % (lerr, loss, ls.item())))
+    for k, p in net.named_parameters():
+        a, b = p.grad.cpu().double(), st[k].grad.double()
+        rel = ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
+        mx = (a - b).abs().max().item() / max(b.abs().max().item(), 1e-30)
+        rows.append((rel <= 1e-3 and mx <= 1e-3, 'grad %s: rel L2 %.3g, max %.3g of max' % (k, rel, mx)))
+    _report(rows)
+
+
+def _train_step_with(net, g, x, mask, pwl):
+    dev = torch.device('cuda', 0)
+    out = net(torch.from_numpy(x).to(dev))
+    assert tuple(out.shape) == tuple(g['out_shape'])
+    vec = torch.from_numpy(g['vec']).to(dev)
+    loss = hl.cross_entropy(out[:, 0:1], torch.from_numpy(mask).to(dev), torch.from_numpy(pwl).to(dev),
+                            method='pixel') + hl.MSELoss(out[:, 2:], vec)
+    loss.backward()
+    torch.cuda.synchronize()
+    return out.detach().cpu(), float(loss.item())

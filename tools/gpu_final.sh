@@ -6,7 +6,7 @@
 # GPU step has its own limit; the script stops at the first failure.
 #   bash tools/gpu_final.sh TAG [TESTS=1]
 set -o pipefail
-TAG=${1:-r03}
+TAG=${1:-r04}
 TESTS=${2:-1}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out; mkdir -p $O
@@ -33,6 +33,7 @@ for C in 2 3; do
     > $O/${TAG}_tl$C.log 2>&1 || { tail -30 $O/${TAG}_tl$C.log; exit 1; }
   db=$(find $O/${TAG}_tl$C -name '*.db' | head -1)
   python3 tools/timeline.py "$db" > $O/${TAG}_timeline_config$C.txt 2>&1 || true
+  python3 tools/kernel_audit.py "$db" > $O/${TAG}_kernel_audit_config$C.txt 2>&1 || true
   head -12 $O/${TAG}_timeline_config$C.txt
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetch$C \
     -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-timing \
@@ -50,14 +51,21 @@ for C in 2 3; do
   find $O/${TAG}_fetch$C $O/${TAG}_write$C $O/${TAG}_prof$C $O/${TAG}_profs$C $O/${TAG}_tl$C -name '*.csv' -size +20M -delete 2>/dev/null
   find $O/${TAG}_tl$C -name '*.db' -delete 2>/dev/null
 done
-# the bench lines cite profiles/r03_* (bench.py PROFILE_TAG): install this
+# config 5 (RDCNet, --runet): kernel stats of its step
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_profrunet \
+  -- python3 bench.py --runet --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing \
+  > $O/${TAG}_profrunet.log 2>&1 || { tail -30 $O/${TAG}_profrunet.log; exit 1; }
+f=$(find $O/${TAG}_profrunet -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_runet.csv
+find $O/${TAG}_profrunet -name '*.csv' -size +20M -delete 2>/dev/null
+# the bench lines cite profiles/<TAG>_* (bench.py PROFILE_TAG): install this
 # pass's summaries there first (in the box's copy; the results come back via
 # gpurun_out/ and are committed from there)
 for C in 2 3; do
-  cp $O/${TAG}_kernel_stats_config$C.csv profiles/r03_kernel_stats_config$C.csv
-  cp $O/${TAG}_kernel_stats_serial_config$C.csv profiles/r03_kernel_stats_serial_config$C.csv
-  [ -s $O/${TAG}_traffic_config$C.json ] && cp $O/${TAG}_traffic_config$C.json profiles/r03_traffic_config$C.json
+  cp $O/${TAG}_kernel_stats_config$C.csv profiles/${TAG}_kernel_stats_config$C.csv
+  cp $O/${TAG}_kernel_stats_serial_config$C.csv profiles/${TAG}_kernel_stats_serial_config$C.csv
+  [ -s $O/${TAG}_traffic_config$C.json ] && cp $O/${TAG}_traffic_config$C.json profiles/${TAG}_traffic_config$C.json
 done
+cp $O/${TAG}_kernel_stats_runet.csv profiles/${TAG}_kernel_stats_runet.csv
 for C in 2 3; do
   timeout -k 10 300 python -u bench.py --config $C --steps 20 --warmup 3 > $O/${TAG}_bench_config$C.json 2> $O/${TAG}_bench_config$C.err \
     || { tail -30 $O/${TAG}_bench_config$C.err; exit 1; }
