@@ -385,7 +385,7 @@ def runet_main(args):
             lr['kernels'][kk] = round(lr['kernels'].get(kk, 0.0) + v['ms'] * 1e3 / args.steps, 2)
         layers = sorted(({"layer": r['layer'], "measured_us": round(r['us'], 2), "launches": r['launches'],
                           "gflop": round(r['gflop'], 4),
-                          "tflops": round(r['gflop'] / r['us'] * 1e-3, 2) if r['us'] else None,
+                          "tflops": round(r['gflop'] / r['us'] * 1e3, 2) if r['us'] else None,
                           "kernels": r['kernels']} for r in per_layer.values()),
                         key=lambda r: -r['measured_us'])
         total_ms = sum(v['ms'] for v in rep.values())

@@ -589,11 +589,13 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
 // ---------------------------------------------------------------------------
 // CUs' worth of resident workgroups the bf16 weight gradient is sized for
 // (HCU_BW_CUS, A/B): fewer voxel blocks write fewer fp32 slabs for the
-// finalize to read, and leave the chain's kernels room on the CUs.
+// finalize to read, and leave the chain's kernels room on the CUs.  Config 3
+// (interleaved A/B, 2 runs each): 256 -> 6.77 ms/step, 224 -> 6.63, 192 ->
+// 6.65, 160 -> 6.81.
 static int bw_cus() {
   static const int v = [] {
     const char *e = getenv("HCU_BW_CUS");
-    const int n = e ? atoi(e) : 256;
+    const int n = e ? atoi(e) : 224;
     return n < 16 ? 16 : (n > 256 ? 256 : n);
   }();
   return v;
