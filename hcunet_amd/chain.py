@@ -45,6 +45,7 @@ class ChainSpec(ctypes.Structure):
         ("ops", ChainOp * MAX_OPS),
         ("bn_eps", ctypes.c_float), ("bn_momentum", ctypes.c_float),
         ("compute_dtype", ctypes.c_int),
+        ("in_cl", ctypes.c_int), ("out_cl", ctypes.c_int), ("in_part_channels", ctypes.c_int),
     ]
 
 
@@ -154,10 +155,16 @@ class Chain:
     ('conv', nn.Conv3d, bn or None, cat_fold) / ('pool', kernel) /
     ('convt', nn.ConvTranspose3d)."""
 
-    def __init__(self, flat, in_channels, ops, name=''):
+    def __init__(self, flat, in_channels, ops, name='', in_cl=False, out_cl=False, in_part=0):
+        """in_cl / out_cl: the input / output is a channels-last tensor
+        [B, X, Y, Z, Cs] of the compute dtype (cl_channels(C)) instead of
+        NCXYZ: consecutive chains then hand their activations over without a
+        layout pass.  in_part: the input is torch.cat(..., dim=-1) of such
+        tensors with in_part channels each (include/hcunet.h)."""
         if not 1 <= len(ops) <= MAX_OPS:
             raise ValueError('a chain has 1..%d ops' % MAX_OPS)
         self.name = name
+        self.in_cl, self.out_cl, self.in_part = bool(in_cl), bool(out_cl), int(in_part)
         self.flat = flat
         self.in_channels = in_channels
         self.ops = ops
@@ -221,7 +228,14 @@ class Chain:
         s.bn_eps = eps
         s.bn_momentum = -1.0 if mom is None else mom
         s.compute_dtype = _lib.HCU_BF16 if bf16 else _lib.HCU_F32
+        s.in_cl, s.out_cl, s.in_part_channels = int(self.in_cl), int(self.out_cl), self.in_part
         return s
+
+    def in_cs(self, bf16):
+        """Channel stride of a channels-last input (the parts padded on their own)."""
+        if self.in_part:
+            return self.in_channels // self.in_part * cl_channels(self.in_part, bf16)
+        return cl_channels(self.in_channels, bf16)
 
     def _offsets(self):
         mods = [m for op in self.ops for m in op[1:] if isinstance(m, nn.Module)]
@@ -232,9 +246,15 @@ class Chain:
         key = (tuple(shape), bool(bf16), self._offsets())
         p = self.plans.get(key)
         if p is None:
-            B, C, X, Y, Z = shape
-            if C != self.in_channels:
-                raise RuntimeError('expected input with %d channels, got %d' % (self.in_channels, C))
+            if self.in_cl:
+                B, X, Y, Z, C = shape
+                if C != self.in_cs(bf16):
+                    raise RuntimeError('expected a channels-last input with %d channel slots, got %d'
+                                       % (self.in_cs(bf16), C))
+            else:
+                B, C, X, Y, Z = shape
+                if C != self.in_channels:
+                    raise RuntimeError('expected input with %d channels, got %d' % (self.in_channels, C))
             p = _ChainPlan(self.spec(bf16), B, X, Y, Z)
             self.plans[key] = p
         return p
@@ -258,7 +278,11 @@ class Chain:
         if x.dim() != 5:
             raise RuntimeError('Expected 5D input [B, C, X, Y, Z] for conv3d, got %dD' % x.dim())
         ok = (torch.float32, torch.float16, torch.bfloat16) if bf16 else (torch.float32, torch.float16)
-        if x.dtype not in ok:
+        if self.in_cl:
+            ok = (torch.bfloat16,) if bf16 else (torch.float32,)
+            if x.dtype not in ok:
+                x = x.to(ok[0])
+        elif x.dtype not in ok:
             x = x.float()
         return _ChainFunction.apply(x, self, bool(training), bool(bf16), *params)
 
@@ -311,7 +335,12 @@ class _ChainFunction(torch.autograd.Function):
         x = x.contiguous()
         plan = chain.plan(x.shape, bf16)
         dev = x.device
-        out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
+        if chain.out_cl:
+            B, C, X, Y, Z = plan.out_shape
+            out = torch.empty((B, X, Y, Z, cl_channels(C, bf16)), dtype=torch.bfloat16 if bf16 else torch.float32,
+                              device=dev)
+        else:
+            out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
         saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
         t = _tensors(chain, x, out, saved, scratch)
@@ -323,7 +352,7 @@ class _ChainFunction(torch.autograd.Function):
                                            _lib.stream_handle(dev)), 'chain forward')
         if TAG_CHAINS:
             L.hcu_timing_prefix(b'')
-        ctx.chain, ctx.plan, ctx.training = chain, plan, training
+        ctx.chain, ctx.plan, ctx.training, ctx.bf16 = chain, plan, training, bf16
         ctx.save_for_backward(x, saved)
         return out
 
@@ -333,9 +362,14 @@ class _ChainFunction(torch.autograd.Function):
         x, saved = ctx.saved_tensors
         chain, plan = ctx.chain, ctx.plan
         dev = x.device
-        dout = dout.contiguous().float()
+        if chain.out_cl:   # the gradient slots' layout and precision
+            dout = dout.contiguous().to(torch.bfloat16 if ctx.bf16 else torch.float32)
+        else:
+            dout = dout.contiguous().float()
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
-        dx = torch.empty(x.shape, dtype=torch.float32, device=dev) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(x.shape, dtype=x.dtype if chain.in_cl else torch.float32, device=dev)
         G, finish = chain.flat.grad_target()
         t = _tensors(chain, x, None, saved, scratch, grads=G)
         L = _lib.lib()
@@ -352,6 +386,13 @@ class _ChainFunction(torch.autograd.Function):
         if dx is not None and dx.dtype != x.dtype:
             dx = dx.to(x.dtype)
         return (dx, None, None, None) + (None,) * len(chain.flat.params)
+
+
+def cl_channels(c, bf16):
+    """Channel slots of a channels-last chain tensor: c rounded up to the
+    16-byte vector (8 bf16 / 4 fp32 channels), padding zero."""
+    v = 8 if bf16 else 4
+    return (c + v - 1) // v * v
 
 
 def flat_of(module, root=None):

@@ -635,6 +635,7 @@ struct WGradFinalize {
               // 3 ConvTranspose3d in the phase form (WGradArgs::nph): row (j, ci), column
               // (q, co) -> dW[ci][co][t], t = (J-1-j)*S + q per dimension; db[co] = sum_q bias row
   int Cout, Cin_g, groups, fold_mod, ACs;   // conv
+  int part_c, part_cs;   // conv input made of channel parts (0: none; prep_all.hip weff2)
   int Cin, CoutT, GCs;                      // convT
   int J[3], SS[3];                          // mode 3: taps per phase, stride
   int accumulate;

@@ -28,8 +28,15 @@ __device__ __forceinline__ bool prep_index2(const WPack &pk, uint32_t i, int T, 
 }
 
 // Effective (folded, block-diagonal) Conv3d weight element W_eff[o][e][t].
+// part_cs > 0: the input is made of channel parts (ConvLayer::part_c): packed
+// channel e is torch channel (e / part_cs) * part_c + e % part_cs, or padding.
 __device__ __forceinline__ float weff2(const float *w, int o, int e, int t, int Cout, int Cin_g,
-                                       int groups, int fold_mod, int T) {
+                                       int groups, int fold_mod, int T, int part_c = 0, int part_cs = 0) {
+  if (part_cs) {
+    const int r = e % part_cs;
+    if (r >= part_c) return 0.f;
+    e = (e / part_cs) * part_c + r;
+  }
   const int g = o / (Cout / groups);
   const int cin_total = groups * Cin_g;
   float s = 0.f;
@@ -63,9 +70,10 @@ __device__ __forceinline__ float prep_eval(const PrepJob &jb, const float *w, in
   const int *p = jb.p;
   switch (jb.kind) {
     case PREP_CONV_FWD:   // (t, e, co)
-      return (b < p[0] && a < p[7]) ? weff2(w, b, a, t, p[0], p[1], p[2], p[3], p[4]) : 0.f;
+      return (b < p[0] && a < p[7]) ? weff2(w, b, a, t, p[0], p[1], p[2], p[3], p[4], p[8], p[9]) : 0.f;
     case PREP_CONV_DGRAD:   // (t', co, e)
-      return (a < p[0] && b < p[7]) ? weff2(w, a, b, p[4] - 1 - t, p[0], p[1], p[2], p[3], p[4]) : 0.f;
+      return (a < p[0] && b < p[7]) ? weff2(w, a, b, p[4] - 1 - t, p[0], p[1], p[2], p[3], p[4], p[8], p[9])
+                                    : 0.f;
     case PREP_CONVT_FUSED: {   // (t, ci, nn)
       const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
       const int sx = p[5], sy = p[6], sz = p[7];
@@ -172,7 +180,7 @@ __device__ void prep_tile(const PrepJob &jb, const float *w, float *dst, float *
 // Whether a job takes the LDS-staged form (host side).
 static bool prep_tiled(const PrepJob &jb, size_t lds_cap_floats) {
   if (jb.kind != PREP_CONV_FWD && jb.kind != PREP_CONV_DGRAD) return false;
-  if (jb.p[2] != 1 || jb.p[3] < 1) return false;                       // groups == 1
+  if (jb.p[2] != 1 || jb.p[3] < 1 || jb.p[9]) return false;           // groups == 1, no parts
   const bool bf = jb.bf16 && jb.pk.on == 3, f32 = !jb.bf16 && jb.pk.on == 1;
   if (!bf && !f32) return false;
   const int V = bf ? 8 : 4;

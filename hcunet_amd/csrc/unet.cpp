@@ -45,11 +45,16 @@ using namespace hcu;
 namespace {
 
 constexpr int kTargetBlocks = 1024;
+bool tails_enabled();   // (BnbFin last-workgroup finalizes, below)
 
 // Activation tensor dims.  es = element bytes: 4 (fp32 path, channel stride a
 // multiple of 4 = 16 bytes) or 2 (bf16 path, channel stride a multiple of 8).
 struct Dims {
   int B = 0, X = 0, Y = 0, Z = 0, C = 0, Cs = 0, es = 4;
+  // > 0: the channels are parts of part_c real channels, each padded to the
+  // vector width on its own (a chain input that is the channel-wise cat of
+  // channels-last chain outputs, hcu_chain_spec::in_part_channels)
+  int part_c = 0;
   int64_t vox() const { return (int64_t)B * X * Y * Z; }
   // 4-byte slots the tensor occupies (buffers are carved in float units)
   size_t floats() const { return ((size_t)vox() * Cs * es + 3) / 4; }
@@ -87,6 +92,7 @@ struct BNLayer {
 struct ConvLayer {
   std::string name;  // layer tag for per-layer timing ("d0.c1", "u3.c2", ...)
   int Cout = 0, Cin_g = 0, groups = 1, fold_mod = 0, E = 0, T = 0;
+  int part_c = 0, part_cs = 0;   // input channel parts (Dims::part_c): packed e <-> torch channel
   int K[3], D[3];
   int S[3] = {1, 1, 1}, P[3] = {0, 0, 0};   // stride, zero padding (chains; the U-Net is valid)
   bool has_dgrad = true;                   // input gradient planned (stride 1)
@@ -182,6 +188,15 @@ WGradArgs wgrad_conv(const Dims &in, const Dims &out, const int K[3], const int 
   return w;
 }
 
+// An input made of channel parts (Dims::part_c): every packed channel e of
+// the input stride is a GEMM row (the padding ones get zero weights), and
+// e maps to torch channel (e / part_cs) * part_c + e % part_cs.
+void set_parts(ConvLayer &L, const Dims &in) {
+  L.part_c = in.part_c;
+  L.part_cs = in.part_c ? round_up(in.part_c, in.es == 2 ? 8 : 4) : 0;
+  if (in.part_c) L.E = in.Cs;
+}
+
 // Conv3d with stride / zero padding (nn.Conv3d(..., stride, padding), the
 // r_unet.py layers): out = floor((in + 2P - D(K-1) - 1) / S) + 1.  Forward:
 // o*S + t*D - P; input gradient (stride 1): the full correlation with padding
@@ -196,6 +211,7 @@ int setup_conv_general(ConvLayer &L, const Dims &in, int Cout, int groups, int f
   L.Cin_g = cin_total / groups;
   L.fold_mod = fold_mod;
   L.E = std::min(fold_mod, cin_total);
+  set_parts(L, in);
   L.T = L.K[0] * L.K[1] * L.K[2];
   L.in = in;
   int o[3];
@@ -264,6 +280,8 @@ int setup_conv_general(ConvLayer &L, const Dims &in, int Cout, int groups, int f
         return fail(HCU_ERR_UNSUPPORTED, std::string(name) + ": sub-lattice output too small");
     }
     L.sub_in = mkdims(in.B * nlat, sub_i[0], sub_i[1], sub_i[2], in.C, in.es);
+    L.sub_in.Cs = in.Cs;
+    L.sub_in.part_c = in.part_c;
     L.sub_out = mkdims(in.B * nlat, sub_o[0], sub_o[1], sub_o[2], Cout, in.es);
     L.fwd = gconv_conv_fwd(L.sub_in, L.sub_out, L.K, one, Cout);
     L.fwd.px = Pd[0]; L.fwd.py = Pd[1]; L.fwd.pz = Pd[2];
@@ -302,6 +320,7 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
   L.Cin_g = cin_total / groups;
   L.fold_mod = fold_mod;
   L.E = std::min(fold_mod, cin_total);
+  set_parts(L, in);
   L.T = K[0] * K[1] * K[2];
   L.in = in;
   const int ox = in.X - D[0] * (K[0] - 1), oy = in.Y - D[1] * (K[1] - 1), oz = in.Z - D[2] * (K[2] - 1);
@@ -522,6 +541,7 @@ struct hcu_unet_plan {
   };
   std::vector<ChainOp> chain;
   bool is_chain = false;
+  bool in_cl = false, out_cl = false;   // chain boundaries in the executor's layout (hcu_chain_spec)
   size_t ufull_off = 0, sub_off[3] = {};   // scratch: full ConvTranspose3d output, sub-lattice temporaries
   size_t max_sub = 0, max_ufull = 0;
   size_t wpart_floats = 0;   // weight-gradient slab arena (deferred, batched finalizes)
@@ -831,7 +851,9 @@ int build_plan(hcu_unet_plan &p) {
   p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
   // one counter block per BatchNorm layer's backward finalize (+ slack)
-  p.n_ctr_sites = fwd_only ? 0 : p.n_bn + 4;
+  // (counters only for the opt-in last-workgroup finalizes: no memset per
+  // backward otherwise)
+  p.n_ctr_sites = fwd_only || !tails_enabled() ? 0 : p.n_bn + 4;
   p.fin_off = scratch.take_floats(std::max<size_t>(16, (size_t)p.n_ctr_sites * kCtrPerSite));
   p.scratch_bytes = scratch.off;
   if (getenv("HCU_PLAN_LOG")) {   // weight-gradient kernels and their partial slabs (measurement)
@@ -1169,6 +1191,8 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   f.Cin_g = L.Cin_g;
   f.groups = L.groups;
   f.fold_mod = L.fold_mod;
+  f.part_c = L.part_c;
+  f.part_cs = L.part_cs;
   f.ACs = w.ACs;
   f.accumulate = accumulate;
   if (int e = c.pend_wgf(f)) return e;   // finalized with the next flush (Ctx::slab / end of backward)
@@ -2122,7 +2146,24 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
   const bool bf = p.es == 2;
   Region saved;
   p.xin = mkdims(p.B, p.X, p.Y, p.Z, cs.in_channels, p.es);
-  p.xcl_off = saved.take_floats(p.xin.floats());
+  p.in_cl = cs.in_cl != 0;
+  p.out_cl = cs.out_cl != 0;
+  if (cs.in_part_channels > 0) {
+    if (!p.in_cl) return fail(HCU_ERR_INVALID, "chain: in_part_channels needs in_cl");
+    if (cs.in_channels % cs.in_part_channels)
+      return fail(HCU_ERR_INVALID, "chain: in_channels must be a multiple of in_part_channels");
+    if (cs.ops[0].kind != HCU_CHAIN_CONV || cs.ops[0].groups != 1 || cs.ops[0].cat_fold)
+      return fail(HCU_ERR_UNSUPPORTED, "chain: an input of channel parts needs a first Conv3d, groups 1");
+    p.xin.part_c = cs.in_part_channels;
+    p.xin.Cs = (cs.in_channels / cs.in_part_channels) * round_up(cs.in_part_channels, bf ? 8 : 4);
+  }
+  if (p.out_cl) {
+    const hcu_chain_op &l = cs.ops[cs.n_ops - 1];
+    if (l.kind != HCU_CHAIN_CONV || l.bn_relu)
+      return fail(HCU_ERR_UNSUPPORTED, "chain: out_cl needs a last Conv3d without BatchNorm");
+  }
+  // (in_cl: the caller's tensor is the first op's input, nothing is copied)
+  p.xcl_off = p.in_cl ? 0 : saved.take_floats(p.xin.floats());
   p.max_act = p.xin.floats();
   p.chain.assign(cs.n_ops, ChainOp{});
   Dims cur = p.xin;
@@ -2251,12 +2292,14 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
   for (ChainOp &o : p.chain) {
     if (o.kind == HCU_CHAIN_CONV) {
       ConvLayer &cl = o.conv;
-      const int pf[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.fwd.ICs, cl.fwd.CoutW,
-                         std::min(cl.fold_mod, cl.groups * cl.Cin_g)};
-      add_job(PREP_CONV_FWD, prep_elems(cl.fwd), cl.w_off, wpack_of(cl.fwd), pf, 8, cl.wf_off);
+      const int pf[10] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.fwd.ICs, cl.fwd.CoutW,
+                          cl.part_c ? cl.fwd.ICs : std::min(cl.fold_mod, cl.groups * cl.Cin_g),
+                          cl.part_c, cl.part_cs};
+      add_job(PREP_CONV_FWD, prep_elems(cl.fwd), cl.w_off, wpack_of(cl.fwd), pf, 10, cl.wf_off);
       if (cl.has_dgrad) {
-        const int pd[8] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.dgrad.ICs, cl.dgrad.CoutW, cl.E};
-        add_job(PREP_CONV_DGRAD, prep_elems(cl.dgrad), cl.w_off, wpack_of(cl.dgrad), pd, 8, cl.wd_off);
+        const int pd[10] = {cl.Cout, cl.Cin_g, cl.groups, cl.fold_mod, cl.T, cl.dgrad.ICs, cl.dgrad.CoutW, cl.E,
+                            cl.part_c, cl.part_cs};
+        add_job(PREP_CONV_DGRAD, prep_elems(cl.dgrad), cl.w_off, wpack_of(cl.dgrad), pd, 10, cl.wd_off);
       }
     } else if (o.kind == HCU_CHAIN_CONVT) {
       ConvTLayer &u = o.ct;
@@ -2304,10 +2347,10 @@ struct ChainAct {
   const float *x = nullptr, *sc = nullptr, *sh = nullptr;
 };
 
-std::vector<ChainAct> chain_inputs(const hcu_unet_plan &p, char *sv, ChainAct *out_act) {
+std::vector<ChainAct> chain_inputs(const hcu_unet_plan &p, char *sv, const void *x, ChainAct *out_act) {
   std::vector<ChainAct> in(p.chain.size());
   ChainAct a;
-  a.x = reinterpret_cast<const float *>(sv + p.xcl_off);
+  a.x = p.in_cl ? reinterpret_cast<const float *>(x) : reinterpret_cast<const float *>(sv + p.xcl_off);
   for (size_t i = 0; i < p.chain.size(); ++i) {
     const ChainOp &o = p.chain[i];
     in[i] = a;
@@ -2333,20 +2376,23 @@ std::vector<ChainAct> chain_inputs(const hcu_unet_plan &p, char *sv, ChainAct *o
 int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training, hipStream_t s) {
   Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   const int es = p.es, bf = c.bf();
-  float *xcl = c.fptr(c.sv, p.xcl_off);
   tag(std::string("chain"), "fwd");
-  if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf, t->x_dtype)) return e;
+  if (!p.in_cl)
+    if (int e = launch_to_cl(t->x, c.fptr(c.sv, p.xcl_off), p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf,
+                             t->x_dtype))
+      return e;
   const std::vector<PrepJob> &jobs = training ? p.prep_jobs : p.prep_fwd;
   if (!jobs.empty())
     if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), jobs.data(), (int)jobs.size(), s)) return e;
   ChainAct last;
-  const std::vector<ChainAct> in = chain_inputs(p, c.sv, &last);
+  const std::vector<ChainAct> in = chain_inputs(p, c.sv, t->x, &last);
   for (size_t i = 0; i < p.chain.size(); ++i) {
     const ChainOp &o = p.chain[i];
     const ChainAct &a = in[i];
     if (o.kind == HCU_CHAIN_CONV) {
       const ConvLayer &L = o.conv;
-      float *y = c.fptr(c.sv, L.y_off);
+      // (out_cl: the last conv writes the caller's tensor; no op of this chain reads it back)
+      float *y = p.out_cl && i + 1 == p.chain.size() ? t->out : c.fptr(c.sv, L.y_off);
       if (L.s2b) {
         float *xs = c.fptr(c.sv, o.xs_off), *ys = c.fptr(c.sc, p.sub_off[0]);
         const int sd[3] = {L.sub_in.X, L.sub_in.Y, L.sub_in.Z}, so[3] = {L.sub_out.X, L.sub_out.Y, L.sub_out.Z};
@@ -2420,9 +2466,10 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
     }
   }
   tag(std::string("chain"), "out");
-  if (int e = launch_from_cl_act(last.x, last.sc, last.sh, t->out, p.B, p.outd.C, p.outd.Cs,
-                                 p.outd.vox() / p.B, s, bf))
-    return e;
+  if (!p.out_cl)
+    if (int e = launch_from_cl_act(last.x, last.sc, last.sh, t->out, p.B, p.outd.C, p.outd.Cs,
+                                   p.outd.vox() / p.B, s, bf))
+      return e;
   if (training && p.n_bn && t->bn_num_batches_tracked)
     if (int e = launch_bn_count_increment(t->bn_num_batches_tracked, p.n_bn, s)) return e;
   if (timing_on()) timing_set_tag("");
@@ -2434,7 +2481,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
   Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   const int es = p.es, bf = c.bf();
   const int n = (int)p.chain.size();
-  const std::vector<ChainAct> in = chain_inputs(p, c.sv, nullptr);
+  const std::vector<ChainAct> in = chain_inputs(p, c.sv, t->x, nullptr);
   // an eval-mode forward prepared only the forward weight images
   if (!training && !p.prep_bwd.empty())
     if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(), s))
@@ -2442,8 +2489,12 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
   int cur = 0;
   if (int e = c.alloc(cur)) return e;
   tag(std::string("chain"), "bwd");
-  if (int e = launch_to_cl(dout, c.buf(cur), p.B, p.outd.C, p.outd.Cs, p.outd.vox() / p.B, s, bf, HCU_F32))
+  if (p.out_cl) {   // dout is already in the layout (and the precision) of the gradient slots
+    HCU_HIP(hipMemcpyAsync(c.buf(cur), dout, (size_t)p.outd.vox() * p.outd.Cs * es, hipMemcpyDeviceToDevice, s));
+  } else if (int e = launch_to_cl(dout, c.buf(cur), p.B, p.outd.C, p.outd.Cs, p.outd.vox() / p.B, s, bf,
+                                  HCU_F32)) {
     return e;
+  }
   bool pre = false;   // buf(cur) already holds d(pre-BatchNorm y) of op i
   for (int i = n - 1; i >= 0; --i) {
     const ChainOp &o = p.chain[i];
@@ -2458,8 +2509,12 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       float *dA = nullptr;
       if (need_dA) {
         if (!L.has_dgrad) return fail(HCU_ERR_UNSUPPORTED, "input gradient of a strided Conv3d");
-        if (int e = c.alloc(sa)) return e;
-        dA = c.buf(sa);
+        if (i == 0 && p.in_cl) {
+          dA = dx;   // the caller's gradient tensor, in the input's layout
+        } else {
+          if (int e = c.alloc(sa)) return e;
+          dA = c.buf(sa);
+        }
       }
       bool done = false;
       if (L.s2b) {
@@ -2481,7 +2536,8 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       }
       if (!need_dA) continue;
       if (i == 0) {
-        if (int e = launch_from_cl(dA, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf)) return e;
+        if (!p.in_cl)
+          if (int e = launch_from_cl(dA, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf)) return e;
       } else {
         cur = sa;
         pre = done;
@@ -2538,8 +2594,11 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       if (!need_dA) continue;
       tag(u.name, "dgrad");
       int sd = 0;
-      if (int e = c.alloc(sd)) return e;
-      float *dP = c.buf(sd);
+      float *dP = dx;   // (i == 0 with in_cl: straight into the caller's gradient tensor)
+      if (!(i == 0 && p.in_cl)) {
+        if (int e = c.alloc(sd)) return e;
+        dP = c.buf(sd);
+      }
       GConvArgs g = u.dgrad;
       g.in = dU;
       g.w = c.fptr(c.sv, u.wd_off);
@@ -2551,7 +2610,8 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       if (fused)
         if (int e = finish_bnbwd(c, g, *bnl, dP, training, accumulate)) return e;
       if (i == 0) {
-        if (int e = launch_from_cl(dP, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf)) return e;
+        if (!p.in_cl)
+          if (int e = launch_from_cl(dP, dx, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, s, bf)) return e;
       } else {
         cur = sd;
         pre = fused;
@@ -2607,6 +2667,8 @@ int hcu_chain_forward(const hcu_unet_plan *p, const hcu_unet_tensors *t, int tra
     return fail(HCU_ERR_INVALID, "null argument");
   if (t->x_dtype != HCU_F32 && t->x_dtype != HCU_F16 && !(t->x_dtype == HCU_BF16 && p->es == 2))
     return fail(HCU_ERR_INVALID, "unsupported input dtype for this plan");
+  if (p->in_cl && t->x_dtype != (p->es == 2 ? HCU_BF16 : HCU_F32))
+    return fail(HCU_ERR_INVALID, "chain: a channels-last input must be of the compute dtype");
   if (training)
     for (const ChainOp &o : p->chain)
       if (o.kind == HCU_CHAIN_CONV && o.bn_relu && o.conv.bn.count <= 1.0)

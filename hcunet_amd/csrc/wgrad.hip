@@ -800,7 +800,13 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
       if (f.db) f.db[o] = f.accumulate ? f.db[o] + v : v;
       return;
     }
-    const int t = grow / f.ACs, e = grow % f.ACs;
+    const int t = grow / f.ACs;
+    int e = grow % f.ACs;
+    if (f.part_cs) {   // channel parts: packed e -> torch channel, padding rows dropped
+      const int r = e % f.part_cs;
+      if (r >= f.part_c) return;
+      e = (e / f.part_cs) * f.part_c + r;
+    }
     const int g = o / (f.Cout / f.groups);
     const int cin_total = f.groups * f.Cin_g;
     for (int cp = e; cp < cin_total; cp += f.fold_mod) {
@@ -858,7 +864,8 @@ __device__ __forceinline__ void wgrad_finalize_tile(const WGradFinalize &f, int 
       int64_t idx;
       if (f.mode == 0) {
         const int c = in / f.T, t = in % f.T;
-        const int e = (col / (f.Cout / f.groups) * f.Cin_g + c) % f.fold_mod;
+        int e = (col / (f.Cout / f.groups) * f.Cin_g + c) % f.fold_mod;
+        if (f.part_cs) e = (e / f.part_c) * f.part_cs + e % f.part_c;   // torch channel -> packed
         idx = (int64_t)(t * f.ACs + e) * f.Ntot + col;
       } else {
         idx = (int64_t)row * f.Ntot + (int64_t)in * f.GCs + col;

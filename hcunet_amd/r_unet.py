@@ -42,13 +42,14 @@ def crop(x, y):
     return torch.empty(0)
 
 
-def _chain(owner, root, name, in_channels, ops):
-    """The chain `name` of `owner` over the flat parameters of `root`."""
+def _chain(owner, root, name, in_channels, ops, **cl):
+    """The chain `name` of `owner` over the flat parameters of `root` (cl:
+    Chain's channels-last boundary options)."""
     cache = owner.__dict__.setdefault('_hcu_chains', {})
     key = (id(root), name)
     ch = cache.get(key)
     if ch is None or ch.flat.root is not root:
-        ch = Chain(flat_of(root), in_channels, ops, '%s.%s' % (type(owner).__name__, name))
+        ch = Chain(flat_of(root), in_channels, ops, '%s.%s' % (type(owner).__name__, name), **cl)
         cache[key] = ch
     return ch
 
@@ -386,19 +387,32 @@ class RDCNet(nn.Module):
         self.compute_dtype = None
 
     def forward(self, x):
+        # The recurrence keeps its state channels-last between the chains
+        # (Chain in_cl / out_cl): the cat(x, y) of r_unet.py:223 and the
+        # StackedDilation cat (:362) are channel-wise cats of padded
+        # channels-last tensors that the next 1x1 convolution reads as channel
+        # parts (in_part), the residual add (:224) is an add of two such
+        # tensors -- no layout pass between the 71 convolutions of a step.
         _ready(x, 'RDCNet input')
         bf16 = bf16_active(self)
         tr = self.training
-        x = _chain(self, self, 'strided', self.strided_conv.in_channels,
-                   [('conv', self.strided_conv, None, False)])(x, tr, bf16)
-        y = None
+        C = self.strided_conv.out_channels
+        blk, sd = self.RDCblock, self.RDCblock.grouped_conv
+        cl = dict(in_cl=True, out_cl=True)
+        x = _chain(self, self, 'strided_cl', self.strided_conv.in_channels,
+                   [('conv', self.strided_conv, None, False)], out_cl=True)(x, tr, bf16)
+        step = _chain(blk, self, 'conv_cl', blk.conv.in_channels, [('conv', blk.conv, None, False)],
+                      in_part=C, **cl)
+        dil = [_chain(sd, self, 'd%d_cl' % i, C, [('conv', c, None, False)], **cl)
+               for i, c in enumerate((sd.conv1, sd.conv2, sd.conv3, sd.conv4, sd.conv5))]
+        mix = _chain(sd, self, 'out_cl', sd.out_conv.in_channels, [('conv', sd.out_conv, None, False)],
+                     in_part=C, **cl)
+        y = torch.zeros_like(x)
         for t in range(10):
-            if t == 0:
-                y = torch.zeros(x.shape, device=x.device)
-            in_ = torch.cat((x, y), dim=1)
-            y = self.RDCblock._run(in_, self, bf16, tr) + y
-        y = _chain(self, self, 'out', self.out_conv.in_channels, [('conv', self.out_conv, None, False)])(
-            y, tr, bf16)
+            h = step(torch.cat((x, y), dim=-1), tr, bf16)
+            y = mix(torch.cat([d(h, tr, bf16) for d in dil], dim=-1), tr, bf16) + y
+        y = _chain(self, self, 'out_cl', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],
+                   in_cl=True)(y, tr, bf16)
         # 5 output channels: no bf16 phase-folded ConvTranspose3d tiling; fp32
         return _chain(self, self, 'convt', self.transposed_conv.in_channels,
                       [('convt', self.transposed_conv)])(y, tr, False)

@@ -200,6 +200,17 @@ typedef struct hcu_chain_spec {
   hcu_chain_op ops[HCU_CHAIN_MAX_OPS];
   float bn_eps, bn_momentum;     /* < 0 momentum: cumulative average (None)   */
   int compute_dtype;             /* HCU_F32 or HCU_BF16 (as hcu_unet_spec)    */
+  /* Channels-last boundaries (the recurrences of hcat/r_unet.py:219-225 keep
+   * their state in the executor's layout between chains instead of NCXYZ):
+   * in_cl / out_cl != 0: t->x / t->out (and dx / dout) are [B][X][Y][Z][Cs]
+   * tensors of the compute dtype, Cs = the channel count rounded up to 8
+   * (bf16) / 4 (fp32), padding channels zero.  in_part_channels > 0 (with
+   * in_cl; the first op a Conv3d): the input is the channel-wise cat of
+   * in_channels / in_part_channels such tensors, each padded on its own
+   * (Cs = parts * round_up(in_part_channels)), i.e. torch.cat(..., dim=-1)
+   * of channels-last chain outputs.  out_cl needs a last op that is a Conv3d
+   * without BatchNorm. */
+  int in_cl, out_cl, in_part_channels;
 } hcu_chain_spec;
 /* Fails with HCU_ERR_SHAPE where torch would raise for the input shape, with
  * HCU_ERR_UNSUPPORTED for op combinations the chain does not run (a MaxPool3d
@@ -208,8 +219,8 @@ int hcu_chain_plan_create(const hcu_chain_spec *spec, int B, int X, int Y, int Z
                           hcu_unet_plan **out);
 int hcu_chain_plan_query(const hcu_unet_plan *plan, int64_t *out_shape, int *n_bn,
                          size_t *saved_bytes, size_t *scratch_bytes);
-/* t->x, t->out: NCXYZ fp32; t->params / t->grads: flat buffers of the op
- * offsets; training as hcu_unet_forward. */
+/* t->x, t->out: NCXYZ fp32 (or channels-last, in_cl / out_cl); t->params /
+ * t->grads: flat buffers of the op offsets; training as hcu_unet_forward. */
 int hcu_chain_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
                       hcu_stream_t stream);
 int hcu_chain_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, const float *dout,

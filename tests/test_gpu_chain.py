@@ -109,3 +109,62 @@ def test_down_pool_chain():
     x = torch.randn((1, 9, 16, 16, 4), generator=torch.Generator().manual_seed(4))
     _check(_run(mods, ['conv', 'bnrelu', 'conv', 'bnrelu', 'pool'], x), rel=1e-4,
            cancelled=('m.0.bias', 'm.2.bias'))
+
+
+def _to_cl(t, cs, dtype):
+    """NCXYZ -> [B, X, Y, Z, cs] with zero padding channels."""
+    v = t.permute(0, 2, 3, 4, 1)
+    return torch.nn.functional.pad(v, (0, cs - t.shape[1])).to(dtype).contiguous()
+
+
+@pytest.mark.parametrize('bf16', [False, True])
+def test_channels_last_boundaries_and_parts(bf16):
+    """Chain in_cl / out_cl / in_part (the RDCNet recurrence's hand-over,
+    include/hcunet.h hcu_chain_spec): a 1x1 Conv3d (2C -> C, C = 10) on the
+    channel-wise cat of two padded channels-last tensors, then a dilated 5^3
+    Conv3d (its sub-lattice form) channels-last in and out, against the same
+    two chains on NCXYZ tensors: outputs, the gradients of both inputs and
+    every weight / bias gradient, to the precision of the compute dtype."""
+    from hcunet_amd.chain import cl_channels
+    torch.manual_seed(3)
+    C = 10
+    c1 = nn.Conv3d(2 * C, C, 1)
+    c2 = nn.Conv3d(C, C, 5, dilation=4, padding=8)
+    shape = (1, C, 40, 36, 12)
+    a = torch.randn(shape)
+    b = torch.randn(shape)
+    g = torch.randn(shape)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    cs = cl_channels(C, bf16)
+    res = {}
+    for mode in ('nc', 'cl'):
+        holder = _Holder(copy.deepcopy(c1), copy.deepcopy(c2)).cuda()
+        flat = FlatParams(holder)
+        m1, m2 = holder.m
+        if mode == 'nc':
+            k1 = Chain(flat, 2 * C, [('conv', m1, None, False)])
+            k2 = Chain(flat, C, [('conv', m2, None, False)])
+            xa, xb = a.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+            y = k2(k1(torch.cat((xa, xb), 1), True, bf16), True, bf16)
+            (y * g.cuda()).sum().backward()
+            res[mode] = (y.detach().cpu(), xa.grad.cpu(), xb.grad.cpu(),
+                         [p.grad.cpu() for p in holder.parameters()])
+        else:
+            k1 = Chain(flat, 2 * C, [('conv', m1, None, False)], in_cl=True, out_cl=True, in_part=C)
+            k2 = Chain(flat, C, [('conv', m2, None, False)], in_cl=True, out_cl=True)
+            xa = _to_cl(a.cuda(), cs, dt).requires_grad_(True)
+            xb = _to_cl(b.cuda(), cs, dt).requires_grad_(True)
+            y = k2(k1(torch.cat((xa, xb), -1), True, bf16), True, bf16)
+            assert y.shape == (1,) + shape[2:] + (cs,) and y.dtype == dt
+            assert not y[..., C:].any()   # padding channels stay zero
+            (y.float() * _to_cl(g.cuda(), cs, torch.float32)).sum().backward()
+            back = lambda t: t[..., :C].float().permute(0, 4, 1, 2, 3).cpu()   # noqa: E731
+            assert not xa.grad[..., C:].any() and not xb.grad[..., C:].any()
+            res[mode] = (back(y.detach()), back(xa.grad), back(xb.grad),
+                         [p.grad.cpu() for p in holder.parameters()])
+    tol = 3e-2 if bf16 else 1e-4
+    (y0, da0, db0, g0), (y1, da1, db1, g1) = res['nc'], res['cl']
+    for name, u, v in [('out', y0, y1), ('dA', da0, da1), ('dB', db0, db1)] + \
+            [('grad%d' % i, u, v) for i, (u, v) in enumerate(zip(g0, g1))]:
+        err = (u.float() - v.float()).abs().max().item()
+        assert err <= tol * max(u.abs().max().item(), 1e-6), (name, err, u.abs().max().item())
