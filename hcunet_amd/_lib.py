@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhcunet.so")
+# HCU_LIB_PATH: a variant build of the same sources (A/B runs, tools/gpu_abx.sh)
+LIB_PATH = os.environ.get("HCU_LIB_PATH") or os.path.join(_HERE, "libhcunet.so")
 
 HCU_OK = 0
 HCU_ERR_INVALID = 1

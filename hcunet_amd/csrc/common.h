@@ -86,13 +86,16 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// CUs' worth of resident workgroups a weight-gradient launch (the backward's
-// branch stream) is sized for: 256 fills the chip; fewer leave slots for the
-// chain stream's kernels to start while the branch runs (HCU_SIDE_CUS, A/B).
+// CUs' worth of resident workgroups an fp32 weight-gradient launch (the
+// backward's branch stream) is sized for: 256 fills the chip; fewer leave
+// slots for the chain stream's kernels to start while the branch runs and
+// write fewer slabs (HCU_SIDE_CUS, A/B).  Config 2, interleaved A/B (2 runs
+// each): 256 -> 2.164 ms/step, 240 -> 2.226, 224 -> 2.150, 192 -> 2.267,
+// 128 -> 2.217 (the grid sizes move the layers' tile partitions).
 inline int side_cus() {
   static const int v = [] {
     const char *e = getenv("HCU_SIDE_CUS");
-    const int n = e ? atoi(e) : 256;
+    const int n = e ? atoi(e) : 224;
     return n < 16 ? 16 : (n > 256 ? 256 : n);
   }();
   return v;
@@ -618,6 +621,8 @@ int plan_wgrad(WGradArgs &a, int target_blocks);
 int plan_wgrad8(WGradArgs &a);
 int launch_wgrad8(const WGradArgs &a, hipStream_t s);
 int launch_wgrad(const WGradArgs &a, hipStream_t s);
+int plan_wgrad3(WGradArgs &a);                 // wgrad3.hip (v2 == 3)
+int launch_wgrad3(const WGradArgs &a, hipStream_t s);
 inline size_t wgrad_partial_floats(const WGradArgs &a) {
   return (size_t)a.KB * a.Mtot * a.Ntot;
 }

@@ -381,7 +381,8 @@ int launch_maxpool_fwd(const float *y, const float *scale, const float *shift,
     const int N = bf ? 8 : 4;
     if (Cs % N == 0) {
       const int64_t nv = (int64_t)B * PX * PY * PZ * (Cs / N);
-      HCU_TIMED(s, "maxpool221_kernel", 0.0, 0.0,
+      // y read, the pooled tensor written
+      HCU_TIMED(s, "maxpool221_kernel", 0.0, (double)(bf ? 2 : 4) * Cs * ((double)B * X * Y * Z + (double)B * PX * PY * PZ),
                 HCU_BF_DISPATCH(bf, maxpool221_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, s,
                                 (const T *)y, scale, shift, (T *)p, X, Y, Z, Cs, PX, PY, (uint32_t)nv,
                                 pool_div(Cs * 4 / N, PX, PY, PZ)));
@@ -481,7 +482,7 @@ bn_bwd_reduce_dense_kernel(T *dA, const T *y, BNCoef coef, int64_t nvox,
 int launch_bn_bwd_reduce_dense(float *dA, const float *y, BNCoef coef, int64_t nvox,
                                int Cs, float *part, int R, hipStream_t s, int bf) {
   const RedGeom g = red_geom(nvox, Cs, R);
-  HCU_TIMED(s, "bn_bwd_reduce_dense_kernel", 0.0, 0.0,
+  HCU_TIMED(s, "bn_bwd_reduce_dense_kernel", 0.0, 2.0 * nvox * Cs * (bf ? 2 : 4),
             HCU_BF_DISPATCH(bf, bn_bwd_reduce_dense_kernel, dim3(R), dim3(256),
                             (size_t)std::max(g.tb, 256) * 8 * 4, s, (T *)dA, (const T *)y, coef,
                             nvox, Cs, part, g));
@@ -694,7 +695,9 @@ int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef, floa
   if (kx == 2 && ky == 2 && kz == 1 && Cs % N == 0) {
     // red_geom over N-channel groups: pass Cs * 4 / N as the "quad" stride
     const RedGeom gv = red_geom((int64_t)B * (X / 2) * (Y / 2) * Z, Cs * 4 / N, R);
-    HCU_TIMED(s, "bn_bwd_reduce_pool221_kernel", 0.0, 0.0,
+    // the pooled gradient and y read, dz written
+    HCU_TIMED(s, "bn_bwd_reduce_pool221_kernel", 0.0,
+              (double)(bf ? 2 : 4) * Cs * ((double)B * (X / 2) * (Y / 2) * Z + 2.0 * B * X * Y * Z),
               HCU_BF_DISPATCH(bf, bn_bwd_reduce_pool221_kernel, dim3(R), dim3(256),
                               (size_t)std::max(gv.tb, 256) * 2 * N * 4, s, (const T *)dP, (const T *)y,
                               coef, (T *)dz, X, Y, Z, Cs, part, gv, pool_div(Cs * 4 / N, X / 2, Y / 2, Z)));
@@ -932,7 +935,8 @@ int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, in
         const int per = G / std::__gcd(256, G);
         grid = std::max(per, grid / per * per);
       }
-      HCU_TIMED(s, "bn_bwd_apply_vec_kernel", 0.0, 0.0,
+      // algorithmic bytes: dz and y read, dY written
+      HCU_TIMED(s, "bn_bwd_apply_vec_kernel", 0.0, 3.0 * nvox * Cs * (bf ? 2 : 4),
                 HCU_BF_DISPATCH(bf, bn_bwd_apply_vec_kernel, dim3(grid), dim3(256), 0, s, (T *)dz,
                                 (const T *)y, coef, nv, G));
       HCU_CHECK_LAUNCH();
@@ -947,7 +951,7 @@ int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, in
     const int per = C4 / std::__gcd(256, C4);   // blocks per period
     grid = std::max(per, grid / per * per);
   }
-  HCU_TIMED(s, "bn_bwd_apply_kernel", 0.0, 0.0,
+  HCU_TIMED(s, "bn_bwd_apply_kernel", 0.0, 3.0 * nvox * Cs * (bf ? 2 : 4),
             HCU_BF_DISPATCH(bf, bn_bwd_apply_kernel, dim3(grid), dim3(256), 0, s,
                             (T *)dz, (const T *)y, coef, n4, Cs / 4));
   HCU_CHECK_LAUNCH();

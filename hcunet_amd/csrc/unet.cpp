@@ -858,7 +858,7 @@ int build_plan(hcu_unet_plan &p) {
   p.scratch_bytes = scratch.off;
   if (getenv("HCU_PLAN_LOG")) {   // weight-gradient kernels and their partial slabs (measurement)
     auto wlog = [](const std::string &n, const WGradArgs &w) {
-      const char *k = w.use_bw ? "bwgrad" : w.v2 == 2 ? "wgrad8" : w.v2 == 1 ? "wgrad2" : "wgrad";
+      const char *k = w.use_bw ? "bwgrad" : w.v2 == 3 ? "wgrad3" : w.v2 == 2 ? "wgrad8" : w.v2 == 1 ? "wgrad2" : "wgrad";
       fprintf(stderr, "wgrad %-8s %-7s KB %5d M %5d N %4d slabs %7.2f MB grid %d x %d x %d\n", n.c_str(), k,
               w.KB, w.Mtot, w.Ntot, 4e-6 * w.KB * (double)w.Mtot * w.Ntot, w.KB, w.mchunks, w.nchunks);
     };

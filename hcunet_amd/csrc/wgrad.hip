@@ -659,6 +659,7 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   long kb = std::max(1L, (long)target_blocks * side_cus() / 256 / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
+  if (a.nph <= 1 && plan_wgrad3(a) == 0) return 0;   // deep layers: the output-split form
   if (a.nph > 1) {   // the phase form runs on wgrad2 only
     if (wgrad2_disabled() || plan_wgrad2(a, target_blocks) != 0)
       return fail(4, "wgrad: no wgrad2 tile for the ConvTranspose3d phase form");
@@ -671,6 +672,7 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
 int launch_wgrad(const WGradArgs &a, hipStream_t s) {
   if (a.use_bw) return launch_bwgrad(a, s);
   if (a.v2 == 2) return launch_wgrad8(a, s);
+  if (a.v2 == 3) return launch_wgrad3(a, s);
   const dim3 grid(a.KB, a.mchunks, a.nchunks);
   const int T = a.KX * a.KY * a.KZ;
   if (a.v2) {

@@ -1,0 +1,356 @@
+// fp32 Conv3d weight gradient for the deep levels, taps on the rows:
+//
+//   dW[(t, ci)][co] = sum_p act(A[p + off(t)][ci]) * G[p][co]   (+ bias row sum_p G[p][co])
+//
+// on v_mfma_f32_16x16x4_f32 (hcat/unet.py:246-257's Conv3d weight gradient).
+// wgrad2 splits a block's voxels over its four waves and reduces them at the
+// end, so a block covers at most 64 rows; with 18 taps that is a 4-channel
+// chunk, and every (tap, channel) chunk re-stages the whole gradient tile (16
+// times on d3.c1 of config 2).  Here the waves split the OUTPUT instead: wave
+// w owns row subtiles w*MS .. w*MS+MS-1 of the block's 64*MS rows (all taps of
+// a 16/32/64-channel chunk) and every voxel of the tile, so a staged voxel
+// tile feeds 64*MS rows x 16*NS columns and no cross-wave reduction is needed.
+//
+// LDS images are channel-major (A: [channel][halo voxel], G: [column][tile
+// voxel]) with row strides = 2 (mod 32): the 16 x 4 lanes of one MFMA operand
+// read (16 channels / columns) x (4 consecutive voxels) with ds_read_b32 on 32
+// distinct banks per half-wave, and a tap is a per-lane voxel offset (no
+// per-tap image copies, no alignment constraint).  Tiles: TX x TY x TZP
+// voxels, TZ the whole (<= 16) Z extent rounded up to a multiple of 4 (the
+// extra z rows read G = 0).  Every block writes one fp32 partial slab
+// [Mtot][Ntot] (the wgrad2 layout); wgrad_finalize sums them in fp64 in a
+// fixed order.
+#include "common.h"
+#include "timing.h"
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace hcu {
+
+bool wgrad3_enabled() {   // HCU_WGRAD3=0 keeps the deep layers on wgrad2 (A/B)
+  static const bool on = [] {
+    const char *e = getenv("HCU_WGRAD3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+constexpr int kW3Loads = 8;   // 16-byte staging loads in flight per thread
+
+template <int MS, int NS>
+__global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kq = lane >> 4, r16 = lane & 15;
+  const int T = a.KX * a.KY * a.KZ;
+  const int CKA = a.CKA, CKG = a.CKG, RSA = a.PA2, RSG = a.PG2;
+  const int tapc = blockIdx.y / a.nci, cic = blockIdx.y % a.nci, coc = blockIdx.z;
+  const int ci0 = cic * CKA, co0 = coc * CKG, t0 = tapc * a.TA;
+  const bool bias_block = a.bias_row && tapc == 0 && cic == 0;
+  const int HAZP = a.HAZP, HAYZ = a.HAY * a.HAZP, TZP = a.TZP;
+  const int HAV = a.HAX * a.HAY * HAZP, PTP = a.TX * a.TY * TZP;
+  float *alds = smem;                                // [CKA + 1][RSA]  (+ zero row)
+  float *glds = alds + (size_t)(CKA + 1) * RSA;      // [CKG + 1][RSG]  (+ zero row)
+  for (int i = tid; i < RSA; i += 256) alds[(size_t)CKA * RSA + i] = 0.f;
+  for (int i = tid; i < RSG; i += 256) glds[(size_t)CKG * RSG + i] = 0.f;
+
+  // this lane's operand bases: A row (tap, channel) of each of the wave's row
+  // subtiles (tap offset in halo voxels folded in), G column of each column
+  // subtile; rows / columns past the layer read the zero rows
+  int aoff[MS];
+#pragma unroll
+  for (int m = 0; m < MS; ++m) {
+    const int r = (wave * MS + m) * 16 + r16;
+    const int tl = r / CKA, c = r % CKA, t = t0 + tl;
+    int off = CKA * RSA;
+    if (tl < a.TA && t < T && ci0 + c < a.ACs) {
+      const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
+      off = c * RSA + kx * a.adx * HAYZ + ky * a.ady * HAZP + kz * a.adz;
+    }
+    aoff[m] = off;
+  }
+  int goff[NS];
+#pragma unroll
+  for (int n = 0; n < NS; ++n) {
+    const int c = n * 16 + r16;
+    goff[n] = (c < CKG && co0 + c < a.GCs) ? c * RSG : CKG * RSG;
+  }
+  floatx4 acc[MS][NS], accb[NS];
+#pragma unroll
+  for (int m = 0; m < MS; ++m)
+#pragma unroll
+    for (int n = 0; n < NS; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int n = 0; n < NS; ++n) accb[n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = bias_block && wave == 0;
+  const bool act = a.a_scale != nullptr;
+  const int CA4 = CKA / 4, CG4 = CKG / 4;
+
+  const int ntiles = a.ntx * a.nty * a.ntz;
+  const int total = a.B * ntiles;
+  const int KBt = (int)gridDim.x, kbi = (int)blockIdx.x;
+  const int tpb = (total + KBt - 1) / KBt;
+  const int t_end = min(total, kbi * tpb + tpb);
+  for (int tt = kbi * tpb; tt < t_end; ++tt) {
+    const int b = tt / ntiles;
+    int tile = tt - b * ntiles;
+    const int tzi = tile % a.ntz;
+    tile /= a.ntz;
+    const int tyi = tile % a.nty, txi = tile / a.nty;
+    const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    lds_barrier();   // the previous tile's operand reads are done
+    // ---- A halo, channel-major (activation applied, 0 outside the input)
+    for (int base = tid; base < HAV * CA4; base += kW3Loads * 256) {
+      float4 val[kW3Loads];
+      int dst[kW3Loads];
+#pragma unroll
+      for (int u = 0; u < kW3Loads; ++u) {
+        const int idx = base + u * 256;
+        val[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[u] = -1;
+        if (idx < HAV * CA4) {
+          const int c4 = idx % CA4, v = idx / CA4;
+          int q, hz, hx, hy;
+          a.fHAZ.divmod(v, q, hz);
+          a.fHAY.divmod(q, hx, hy);
+          dst[u] = c4 * 4 * RSA + v;
+          const int gx = px0 + hx, gy = py0 + hy, gz = pz0 + hz, c = ci0 + c4 * 4;
+          if (gx < a.AX && gy < a.AY && gz < a.AZ && c < a.ACs) {
+            val[u] = *reinterpret_cast<const float4 *>(
+                a.A + ((((size_t)b * a.AX + gx) * a.AY + gy) * a.AZ + gz) * a.ACs + c);
+            if (act) {
+              const float4 sc = *reinterpret_cast<const float4 *>(a.a_scale + c);
+              const float4 sh = *reinterpret_cast<const float4 *>(a.a_shift + c);
+              val[u].x = fmaxf(fmaf(val[u].x, sc.x, sh.x), 0.f);
+              val[u].y = fmaxf(fmaf(val[u].y, sc.y, sh.y), 0.f);
+              val[u].z = fmaxf(fmaf(val[u].z, sc.z, sh.z), 0.f);
+              val[u].w = fmaxf(fmaf(val[u].w, sc.w, sh.w), 0.f);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kW3Loads; ++u) {
+        if (dst[u] < 0) continue;
+        float *d = alds + dst[u];
+        d[0] = val[u].x;
+        d[RSA] = val[u].y;
+        d[2 * RSA] = val[u].z;
+        d[3 * RSA] = val[u].w;
+      }
+    }
+    // ---- G tile, channel-major, z rows of TZP (0 past the output grid)
+    for (int base = tid; base < PTP * CG4; base += kW3Loads * 256) {
+      float4 val[kW3Loads];
+      int dst[kW3Loads];
+#pragma unroll
+      for (int u = 0; u < kW3Loads; ++u) {
+        const int idx = base + u * 256;
+        val[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[u] = -1;
+        if (idx < PTP * CG4) {
+          const int c4 = idx % CG4, p = idx / CG4;
+          const int lz = p % TZP, q = p / TZP;
+          int lx, ly;
+          a.fTY.divmod(q, lx, ly);
+          dst[u] = c4 * 4 * RSG + p;
+          const int gx = px0 + lx, gy = py0 + ly, gz = pz0 + lz, c = co0 + c4 * 4;
+          if (lz < a.TZ && gx < a.PX && gy < a.PY && gz < a.PZ && c < a.GCs)
+            val[u] = *reinterpret_cast<const float4 *>(
+                a.G + ((((size_t)b * a.GX + gx) * a.GY + gy) * a.GZ + gz) * a.GCs + c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kW3Loads; ++u) {
+        if (dst[u] < 0) continue;
+        float *d = glds + dst[u];
+        d[0] = val[u].x;
+        d[RSG] = val[u].y;
+        d[2 * RSG] = val[u].z;
+        d[3 * RSG] = val[u].w;
+      }
+    }
+    lds_barrier();
+    // ---- MFMA over the tile's voxels, 4 per K-step: lane group kq takes voxel
+    // p0 + kq of a z row (halo voxel hv0 + z0 + kq)
+    for (int row = 0; row < a.TX * a.TY; ++row) {
+      int lx, ly;
+      a.fTY.divmod(row, lx, ly);
+      const int hv0 = lx * HAYZ + ly * HAZP + kq, p0 = row * TZP + kq;
+      for (int z0 = 0; z0 < TZP; z0 += 4) {
+        float bv[NS];
+#pragma unroll
+        for (int n = 0; n < NS; ++n) bv[n] = glds[goff[n] + p0 + z0];
+#pragma unroll
+        for (int m = 0; m < MS; ++m) {
+          const float av = alds[aoff[m] + hv0 + z0];
+#pragma unroll
+          for (int n = 0; n < NS; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[n], acc[m][n], 0, 0, 0);
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int n = 0; n < NS; ++n)
+            accb[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, bv[n], accb[n], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- one partial slab per block: each wave writes its own rows
+  const size_t slab = (size_t)blockIdx.x * a.Mtot;
+#pragma unroll
+  for (int m = 0; m < MS; ++m) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int lr = (wave * MS + m) * 16 + kq * 4 + r;
+      const int tl = lr / CKA, t = t0 + tl, ci = ci0 + lr % CKA;
+      if (tl >= a.TA || t >= T || ci >= a.ACs) continue;
+      const int grow = t * a.ACs + ci;
+#pragma unroll
+      for (int n = 0; n < NS; ++n) {
+        const int gcol = co0 + n * 16 + r16;
+        if (n * 16 + r16 < CKG && gcol < a.GCs) a.partial[(slab + grow) * a.Ntot + gcol] = acc[m][n][r];
+      }
+    }
+  }
+  if (do_bias && kq == 0) {   // row 0 of the ones-subtile: sum_p G[p][col]
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+      const int gcol = co0 + n * 16 + r16;
+      if (n * 16 + r16 < CKG && gcol < a.GCs)
+        a.partial[(slab + (size_t)T * a.ACs) * a.Ntot + gcol] = accb[n][0];
+    }
+  }
+}
+
+// Row stride of a channel-major image: >= n, = 2 (mod 32) (see above).
+static int cm_stride(int n) { return n + ((2 - n % 32) + 32) % 32; }
+
+// Plans a Conv3d weight gradient (taps_rows, stride-1 unpadded operands,
+// fp32) for wgrad3_kernel; 0 when it applies.  Chooses the channel chunk, the
+// row subtiles per wave (3 / 5 / 9), the voxel tile and the number of voxel
+// blocks by a per-CU time model: MFMA cycles of a block + its staging (~32
+// bytes a cycle) + its slab write, the blocks spread over the CUs the branch
+// stream is sized for (side_cus).
+int plan_wgrad3(WGradArgs &a) {
+  if (!wgrad3_enabled() || !a.taps_rows || a.nph > 1) return 1;
+  if (a.asx != 1 || a.asy != 1 || a.asz != 1 || a.apx || a.apy || a.apz) return 1;
+  if (a.gsx != 1 || a.gsy != 1 || a.gsz != 1 || a.gpx || a.gpy || a.gpz) return 1;
+  // (16-channel inputs stay on wgrad2: d2.c1 of config 2 ran 65 us here
+  // against 52 us there; every wider layer measured faster here)
+  if (a.ACs % 32 || a.GCs % 32 || a.g_y) return 1;
+  const int T = a.KX * a.KY * a.KZ;
+  const int ntz = cdiv(a.PZ, 16), TZ = cdiv(a.PZ, ntz), TZP = round_up(TZ, 4);
+  const int HAZP = TZP + (a.KZ - 1) * a.adz;
+  const int NS = a.GCs % 64 == 0 ? 4 : 2;
+  const int CKG = NS * 16;
+  const int nco = a.GCs / CKG;
+  const int cus = side_cus();
+  const int mss[3] = {9, 5, 3};
+  const int ckas[3] = {64, 32, 16};
+  const int txys[4][2] = {{4, 4}, {4, 2}, {2, 4}, {2, 2}};
+  double best = 1e300;
+  WGradArgs bestA = a;
+  for (int ci = 0; ci < 3; ++ci) {
+    const int CKA = ckas[ci];
+    if (a.ACs % CKA) continue;
+    for (int mi = 0; mi < 3; ++mi) {
+      const int MS = mss[mi];
+      const int rows = 64 * MS;
+      const int TA = std::min(T, rows / CKA);
+      if (TA < 1) continue;
+      const int ntc = cdiv(T, TA), nci = a.ACs / CKA;
+      const int used = TA * CKA;                   // useful rows of a block (the last tap chunk may be short)
+      if (used * 3 < rows * 2 && MS > 3) continue;   // > 1/3 of the rows idle: a smaller MS fits better
+      for (int ti = 0; ti < 4; ++ti) {
+        const int TX = std::min(txys[ti][0], a.PX), TY = std::min(txys[ti][1], a.PY);
+        const int HAX = TX + (a.KX - 1) * a.adx, HAY = TY + (a.KY - 1) * a.ady;
+        const int HAV = HAX * HAY * HAZP, PTP = TX * TY * TZP;
+        const int RSA = cm_stride(HAV), RSG = cm_stride(PTP);
+        const long lds = ((long)(CKA + 1) * RSA + (long)(CKG + 1) * RSG) * 4;
+        if (lds > 150 * 1024) continue;
+        // two resident blocks (LDS <= 80 KB) overlap one's staging with the
+        // other's MFMAs; one block pays both
+        const int occ = lds <= 80 * 1024 ? 2 : 1;
+        const long tiles = (long)a.B * cdiv(a.PX, TX) * cdiv(a.PY, TY) * ntz;
+        const long per = (long)ntc * nci * nco;
+        const long kb = std::max(1L, std::min(tiles, (long)cus * occ / per));
+        const long tpb = cdiv((int)tiles, (int)kb);
+        const double mfma = (double)PTP / 4 * (MS * NS * 32.0 + 150.0);
+        // staging: ~16 B a cycle per CU plus ~2500 cycles of latency per round
+        // of kW3Loads loads in flight
+        const double f4 = ((double)HAV * CKA + (double)PTP * CKG) / 4;
+        const double stage = f4 * 16 / 16.0 + 2500.0 * std::ceil(f4 / (256.0 * kW3Loads));
+        const double slab = (double)rows * CKG * 4 / 16.0;
+        const long blocks = kb * per;
+        const double rounds = std::ceil((double)blocks / ((double)cus * occ));
+        const double tile_t = occ == 2 ? std::max(mfma, stage) * 1.15 * 2 : mfma + stage;
+        const double cost = rounds * (tpb * tile_t + slab);
+        // the finalize reads every slab once: ~3.3 KB a cycle chip-wide
+        const double fin = (double)blocks * (used + 1) * CKG * 4 / 3300.0;
+        if (cost + fin < best) {
+          best = cost + fin;
+          WGradArgs c = a;
+          c.CKA = CKA;
+          c.CKG = CKG;
+          c.MS = MS;
+          c.NS = NS;
+          c.TA = TA;
+          c.TG = 1;
+          c.ntc = ntc;
+          c.nci = nci;
+          c.nco = nco;
+          c.mchunks = ntc * nci;
+          c.nchunks = nco;
+          c.TX = TX;
+          c.TY = TY;
+          c.TZ = TZ;
+          c.TZP = TZP;
+          c.HAX = HAX;
+          c.HAY = HAY;
+          c.HAZP = HAZP;
+          c.PA2 = RSA;
+          c.PG2 = RSG;
+          c.ntx = cdiv(a.PX, TX);
+          c.nty = cdiv(a.PY, TY);
+          c.ntz = ntz;
+          c.KB = (int)kb;
+          c.lds_bytes = (int)lds;
+          c.fHAZ = FastDiv(HAZP);
+          c.fHAY = FastDiv(HAY);
+          c.fTY = FastDiv(TY);
+          c.v2 = 3;
+          bestA = c;
+        }
+      }
+    }
+  }
+  if (bestA.v2 != 3) return 1;
+  a = bestA;
+  a.Mtot = T * a.ACs + (a.bias_row ? 1 : 0);
+  a.Ntot = a.GCs;
+  return 0;
+}
+
+int launch_wgrad3(const WGradArgs &a, hipStream_t s) {
+  const dim3 grid(a.KB, a.mchunks, a.nchunks);
+  const int T = a.KX * a.KY * a.KZ;
+  const double fl = a.flops > 0 ? a.flops : 2.0 * a.B * a.PX * a.PY * a.PZ * (double)T * a.ACs * a.GCs;
+  const double by = 4.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs + (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
+  bool ok = false;
+#define W3(MS_, NS_)                                                                       \
+  if (!ok && a.MS == MS_ && a.NS == NS_) {                                                 \
+    HCU_TIMED(s, "wgrad3_kernel<" #MS_ "," #NS_ ">", fl, by,                                \
+              HCU_LAUNCH((wgrad3_kernel<MS_, NS_>), grid, dim3(256), a.lds_bytes, s, a)); \
+    ok = true;                                                                             \
+  }
+  W3(3, 2) W3(5, 2) W3(9, 2) W3(3, 4) W3(5, 4) W3(9, 4)
+#undef W3
+  if (!ok) return fail(4, "wgrad3: unsupported variant");
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace hcu

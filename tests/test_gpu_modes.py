@@ -156,6 +156,21 @@ def test_tiled_weight_gradient_finalize(tmp_path):
             assert (a - b).abs().max().item() <= tol
 
 
+def test_output_split_weight_gradient_matches_wgrad2(tmp_path):
+    """wgrad3 (the deep fp32 layers' weight gradient with the waves splitting
+    the output rows, wgrad3.hip) against wgrad2 (HCU_WGRAD3=0) on the same
+    steps: outputs bitwise (the forward does not change), every gradient to
+    fp32 reassociation of the voxel sums (1e-5 of each tensor's largest
+    element, plus 1e-6 absolute for the BatchNorm-cancelled conv biases)."""
+    a = _run(tmp_path, 'w2', {'HCU_WGRAD3': '0'})
+    b = _run(tmp_path, 'w3', {})
+    for it in range(3):
+        assert torch.equal(a[it][0], b[it][0])
+        for k, (x, y) in enumerate(zip(a[it], b[it])):
+            tol = 1e-5 * x.abs().max().item() + 1e-6
+            assert (x - y).abs().max().item() <= tol, (it, k, (x - y).abs().max().item(), tol)
+
+
 OPT_IN = {'HCU_AP': '1', 'HCU_BNB_TAIL': '1', 'HCU_CONVT_PHASE_WG': '1', 'HCU_PREP_TILED': '1'}
 
 
