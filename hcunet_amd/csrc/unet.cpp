@@ -452,10 +452,14 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     max_part = std::max(max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
   }
   u.wg_phase = false;
-  // opt-in (HCU_CONVT_PHASE_WG=1): measured +13 us per config-2 step against the
-  // per-tap wgrad_kernel + chansum (its wider slabs double the finalize reads)
-  static const bool phase_on = getenv("HCU_CONVT_PHASE_WG") && getenv("HCU_CONVT_PHASE_WG")[0] == '1';
-  if (!bf && u.fused && o % 4 == 0 && phase_on) {
+  // The weight gradient of the phase-folded forward (stride phases as extra
+  // output columns): on wgrad3 by default, its bias from chansum (the mode-3
+  // finalize's serial bias sum over the phases is slow); HCU_CONVT_PHASE_WG=1:
+  // on wgrad2 with the bias row (measured +13 us per config-2 step against
+  // the per-tap wgrad_kernel + chansum: its wider slabs double the finalize
+  // reads), =0: off.
+  static const int phase_mode = getenv("HCU_CONVT_PHASE_WG") ? atoi(getenv("HCU_CONVT_PHASE_WG")) : 2;
+  if (!bf && u.fused && o % 4 == 0 && phase_mode) {
     // dW'[(j, ci)][(q, co)] = sum_o A[o + j - (J-1)][ci] * dU[o*S + q][co] over the
     // phase grid o (the forward's fused GEMM, hcat/unet.py:294-298)
     const int J[3] = {u.K[0] / u.S[0], u.K[1] / u.S[1], u.K[2] / u.S[2]};
@@ -471,9 +475,9 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     w.gsx = u.S[0]; w.gsy = u.S[1]; w.gsz = u.S[2];
     w.gdx = w.gdy = w.gdz = 1;
     w.taps_rows = 1;
-    w.bias_row = 1;
+    w.bias_row = phase_mode == 1 ? 1 : 0;
     w.nph = nph; w.phx = u.S[0]; w.phy = u.S[1]; w.phz = u.S[2]; w.GCout = o;
-    if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == 1) {
+    if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == (phase_mode == 1 ? 1 : 3)) {
       u.wgp = w;
       u.wg_phase = true;
       max_part = std::max(max_part, wgrad_partial_floats(w));
@@ -1643,7 +1647,23 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     const BNCoef bp = coef_at(c.sv, prev.bn);
     tag(u.name, "wgrad");
     if (int e = c.fork()) return e;
-    if (u.wg_phase) {   // weight and bias gradient in one launch (WGradArgs::nph)
+    if (u.wg_phase) {   // the weight gradient in one launch (WGradArgs::nph), bias with it or from chansum
+      if (!u.wgp.bias_row) {
+        const int R = chansum_rows(u.out.vox(), u.out.Cs);
+        float *cs = nullptr;
+        if (int e = c.slab((size_t)R * u.out.Cs, cs)) return e;
+        if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, cs, R, c.wstream(), c.bf())) return e;
+        WGradFinalize fb{};
+        fb.partial = cs;
+        fb.db = c.G + u.b_off;
+        fb.KB = R;
+        fb.Mtot = 1;
+        fb.Ntot = u.out.Cs;
+        fb.mode = 2;
+        fb.Cout = u.Cout;
+        fb.accumulate = accumulate;
+        if (int e = c.pend_wgf(fb)) return e;
+      }
       WGradArgs w = u.wgp;
       w.A = c.fptr(c.sv, prev.y_off);
       w.a_scale = bp.scale;
@@ -1654,7 +1674,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       WGradFinalize f{};
       f.partial = w.partial;
       f.dw = c.G + u.w_off;
-      f.db = c.G + u.b_off;
+      f.db = w.bias_row ? c.G + u.b_off : nullptr;
       f.KB = w.KB;
       f.Mtot = w.Mtot;
       f.Ntot = w.Ntot;

@@ -659,7 +659,7 @@ int plan_wgrad(WGradArgs &a, int target_blocks) {
   long kb = std::max(1L, (long)target_blocks * side_cus() / 256 / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
-  if (a.nph <= 1 && plan_wgrad3(a) == 0) return 0;   // deep layers: the output-split form
+  if (plan_wgrad3(a) == 0) return 0;   // deep layers / ConvTranspose3d phase form: the output-split form
   if (a.nph > 1) {   // the phase form runs on wgrad2 only
     if (wgrad2_disabled() || plan_wgrad2(a, target_blocks) != 0)
       return fail(4, "wgrad: no wgrad2 tile for the ConvTranspose3d phase form");

@@ -74,7 +74,17 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
 #pragma unroll
   for (int n = 0; n < NS; ++n) {
     const int c = n * 16 + r16;
-    goff[n] = (c < CKG && co0 + c < a.GCs) ? c * RSG : CKG * RSG;
+    goff[n] = (c < CKG && co0 + c < a.Ntot) ? c * RSG : CKG * RSG;
+  }
+  // ConvTranspose3d phase form (WGradArgs::nph): the block's columns lie in
+  // one stride phase q; G is read at o*S + q, channel co0 - q*GCout
+  int gq[3] = {0, 0, 0}, gcb = co0;
+  if (a.nph > 1) {
+    const int q = co0 / a.GCout;
+    gcb = co0 - q * a.GCout;
+    gq[2] = q % a.phz;
+    gq[1] = (q / a.phz) % a.phy;
+    gq[0] = q / (a.phz * a.phy);
   }
   floatx4 acc[MS][NS], accb[NS];
 #pragma unroll
@@ -115,8 +125,9 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
           a.fHAZ.divmod(v, q, hz);
           a.fHAY.divmod(q, hx, hy);
           dst[u] = c4 * 4 * RSA + v;
-          const int gx = px0 + hx, gy = py0 + hy, gz = pz0 + hz, c = ci0 + c4 * 4;
-          if (gx < a.AX && gy < a.AY && gz < a.AZ && c < a.ACs) {
+          const int gx = px0 + hx - a.apx, gy = py0 + hy - a.apy, gz = pz0 + hz - a.apz, c = ci0 + c4 * 4;
+          if ((unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY && (unsigned)gz < (unsigned)a.AZ &&
+              c < a.ACs) {
             val[u] = *reinterpret_cast<const float4 *>(
                 a.A + ((((size_t)b * a.AX + gx) * a.AY + gy) * a.AZ + gz) * a.ACs + c);
             if (act) {
@@ -155,8 +166,10 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
           int lx, ly;
           a.fTY.divmod(q, lx, ly);
           dst[u] = c4 * 4 * RSG + p;
-          const int gx = px0 + lx, gy = py0 + ly, gz = pz0 + lz, c = co0 + c4 * 4;
-          if (lz < a.TZ && gx < a.PX && gy < a.PY && gz < a.PZ && c < a.GCs)
+          const int ox = px0 + lx, oy = py0 + ly, oz = pz0 + lz, c = gcb + c4 * 4;
+          const int gx = ox * a.gsx + gq[0], gy = oy * a.gsy + gq[1], gz = oz * a.gsz + gq[2];
+          if (lz < a.TZ && ox < a.PX && oy < a.PY && oz < a.PZ && gx < a.GX && gy < a.GY && gz < a.GZ &&
+              c < a.GCs && co0 + c4 * 4 < a.Ntot)
             val[u] = *reinterpret_cast<const float4 *>(
                 a.G + ((((size_t)b * a.GX + gx) * a.GY + gy) * a.GZ + gz) * a.GCs + c);
         }
@@ -211,7 +224,7 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
         const int gcol = co0 + n * 16 + r16;
-        if (n * 16 + r16 < CKG && gcol < a.GCs) a.partial[(slab + grow) * a.Ntot + gcol] = acc[m][n][r];
+        if (n * 16 + r16 < CKG && gcol < a.Ntot) a.partial[(slab + grow) * a.Ntot + gcol] = acc[m][n][r];
       }
     }
   }
@@ -235,18 +248,23 @@ static int cm_stride(int n) { return n + ((2 - n % 32) + 32) % 32; }
 // bytes a cycle) + its slab write, the blocks spread over the CUs the branch
 // stream is sized for (side_cus).
 int plan_wgrad3(WGradArgs &a) {
-  if (!wgrad3_enabled() || !a.taps_rows || a.nph > 1) return 1;
-  if (a.asx != 1 || a.asy != 1 || a.asz != 1 || a.apx || a.apy || a.apz) return 1;
-  if (a.gsx != 1 || a.gsy != 1 || a.gsz != 1 || a.gpx || a.gpy || a.gpz) return 1;
+  if (!wgrad3_enabled() || !a.taps_rows) return 1;
+  const bool ph = a.nph > 1;   // ConvTranspose3d phase form: A padded, G strided by the phases
+  if (a.asx != 1 || a.asy != 1 || a.asz != 1 || a.gpx || a.gpy || a.gpz) return 1;
+  if (!ph && (a.apx || a.apy || a.apz || a.gsx != 1 || a.gsy != 1 || a.gsz != 1)) return 1;
+  if (ph && a.bias_row) return 1;   // (its bias comes from chansum)
   // (16-channel inputs stay on wgrad2: d2.c1 of config 2 ran 65 us here
   // against 52 us there; every wider layer measured faster here)
-  if (a.ACs % 32 || a.GCs % 32 || a.g_y) return 1;
+  if (a.ACs % 32 || a.g_y) return 1;
   const int T = a.KX * a.KY * a.KZ;
   const int ntz = cdiv(a.PZ, 16), TZ = cdiv(a.PZ, ntz), TZP = round_up(TZ, 4);
   const int HAZP = TZP + (a.KZ - 1) * a.adz;
-  const int NS = a.GCs % 64 == 0 ? 4 : 2;
+  const int ncols = ph ? a.nph * a.GCout : a.GCs;
+  const int cw = ph ? a.GCout : a.GCs;   // a column chunk stays inside one phase
+  if (cw % 32) return 1;
+  const int NS = cw % 64 == 0 ? 4 : 2;
   const int CKG = NS * 16;
-  const int nco = a.GCs / CKG;
+  const int nco = ncols / CKG;
   const int cus = side_cus();
   const int mss[3] = {9, 5, 3};
   const int ckas[3] = {64, 32, 16};
@@ -330,7 +348,7 @@ int plan_wgrad3(WGradArgs &a) {
   if (bestA.v2 != 3) return 1;
   a = bestA;
   a.Mtot = T * a.ACs + (a.bias_row ? 1 : 0);
-  a.Ntot = a.GCs;
+  a.Ntot = ncols;
   return 0;
 }
 
