@@ -269,6 +269,8 @@ int plan_wgrad3(WGradArgs &a) {
   const int mss[3] = {9, 5, 3};
   const int ckas[3] = {64, 32, 16};
   const int txys[4][2] = {{4, 4}, {4, 2}, {2, 4}, {2, 2}};
+  // HCU_W3_TILES: bit mask of the tiles offered (A/B)
+  static const int tile_mask = getenv("HCU_W3_TILES") ? atoi(getenv("HCU_W3_TILES")) : 15;
   double best = 1e300;
   WGradArgs bestA = a;
   for (int ci = 0; ci < 3; ++ci) {
@@ -283,6 +285,7 @@ int plan_wgrad3(WGradArgs &a) {
       const int used = TA * CKA;                   // useful rows of a block (the last tap chunk may be short)
       if (used * 3 < rows * 2 && MS > 3) continue;   // > 1/3 of the rows idle: a smaller MS fits better
       for (int ti = 0; ti < 4; ++ti) {
+        if (!((tile_mask >> ti) & 1)) continue;
         const int TX = std::min(txys[ti][0], a.PX), TY = std::min(txys[ti][1], a.PY);
         const int HAX = TX + (a.KX - 1) * a.adx, HAY = TY + (a.KY - 1) * a.ady;
         const int HAV = HAX * HAY * HAZP, PTP = TX * TY * TZP;
@@ -349,6 +352,10 @@ int plan_wgrad3(WGradArgs &a) {
   a = bestA;
   a.Mtot = T * a.ACs + (a.bias_row ? 1 : 0);
   a.Ntot = ncols;
+  if (getenv("HCU_CONV2_LOG"))
+    fprintf(stderr, "wgrad3 plan: A%dx%dx%d ACs%d P%dx%dx%d K%dx%dx%d nph%d | CKA%d MS%d NS%d TA%d T%dx%dx%d(%d) KB%d m%d n%d lds%d\n",
+            a.AX, a.AY, a.AZ, a.ACs, a.PX, a.PY, a.PZ, a.KX, a.KY, a.KZ, a.nph, a.CKA, a.MS, a.NS, a.TA, a.TX, a.TY,
+            a.TZ, a.TZP, a.KB, a.mchunks, a.nchunks, a.lds_bytes);
   return 0;
 }
 
