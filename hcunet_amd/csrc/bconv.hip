@@ -241,7 +241,7 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   const int nb16 = cdiv(Nlog, 16);
   const int ntz = cdiv(a.OZ, 16);
   a.TZ = cdiv(a.OZ, ntz);
-  const long lds_cap = env_int_b("HCU_BCONV_LDS_KB", 80) * 1024L;
+  const long lds_cap = 80 * 1024L;   // (96 / 160 KB measured equal: tools/gpu_bb.sh, ab8)
   // Candidate tilings, scored by a simple per-CU time model (cycles):
   //   per (tile, chunk): MFMA S * MPW * NSUB * (16 bf16 | 128 fp32) per wave, staging ~
   //   1200 + 40 per 16-byte element per thread (+ weights when multi-chunk);
@@ -377,7 +377,7 @@ static void bconv_finish(GConvArgs &a, int ntz, int VEC, int fpf) {
   const long tiles = (long)a.ntx * a.nty * a.ntz * a.B;
   const int nchunks = a.ICs / a.CK;
   int ks = 1;
-  const int ks_target = env_int_b("HCU_BCONV_KS_TARGET", 256);
+  const int ks_target = 256;   // (512 measured +7 % on config 2)
   if (a.nph == 1 && 256 % (a.OCs / VEC) == 0)
     while (ks < nchunks && tiles * nN * ks < ks_target) ks *= 2;
   ks = std::min(ks, nchunks);

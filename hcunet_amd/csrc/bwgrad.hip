@@ -607,13 +607,10 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   (void)target_blocks;
   if (a.ACs % 8 || a.GCs % 8) return fail(4, "bwgrad: channel strides must be multiples of 8");
   if (a.PX <= 0 || a.PY <= 0 || a.PZ <= 0) return fail(2, "bwgrad: empty grid");
-  // channel chunks: A side up to 32 channels (HCU_BW_CKA: a larger cap where
-  // the tile still fits LDS, experiments), G side up to 64 (16-col subtiles)
-  const int cka_cap = getenv("HCU_BW_CKA") ? atoi(getenv("HCU_BW_CKA")) : 32;
-  const WGradArgs in = a;
-  if (cka_cap > 32 && plan_bwgrad_cka(a, cka_cap) == 0) return 0;
-  a = in;
-  return plan_bwgrad_cka(a, std::min(cka_cap, 32));
+  // channel chunks: A side up to 32 channels, G side up to 64 (16-col
+  // subtiles).  (16-channel A chunks measured 7.11 vs 6.63 ms per config-3
+  // step; 64-channel ones fit the LDS of almost no layer.)
+  return plan_bwgrad_cka(a, 32);
 }
 
 static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
@@ -686,7 +683,7 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
     return ((long)a.HAV * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
   };
   // the first tile whose image fits two blocks per CU, else the smallest
-  const int t0i = getenv("HCU_BW_TILE") ? std::max(0, std::min(1, atoi(getenv("HCU_BW_TILE")))) : 0;
+  const int t0i = 0;   // (starting at the 4 x 8 tile measured equal)
   const int nti = 2;
   int pick = -1;
   long best_lds = 1L << 40;
@@ -698,7 +695,7 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   if (pick < -1) pick = -2 - pick;
   if (pick < 0) pick = t0i;
   const long lds = set_tile(pick);
-  if (lds > 160 * 1024) return cka_cap > 32 ? 4 : fail(4, "bwgrad: tile does not fit LDS");
+  if (lds > 160 * 1024) return fail(4, "bwgrad: tile does not fit LDS");
   a.lds_bytes = (int)((lds + 15) & ~15L);
   a.fHAZ = FastDiv(a.HAZ);
   a.fHAY = FastDiv(a.HAY);
@@ -717,11 +714,10 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   const int nA = cdiv(a.HAV, 256 / (a.CKA / 8)), nG = cdiv(a.HGV, 256 / (a.CKG / 8));
   const int np = std::max(nA, nG);
   a.NPA = a.NPG = np <= 8 ? 8 : np <= 16 ? 16 : np <= 32 ? 32 : 0;
-  if (getenv("HCU_BWGRAD_SERIAL")) a.NPA = a.NPG = 0;   // A/B: the serial kernel
   // One fp32 slab per block: the pipelined kernel hides its loads behind the
   // MFMAs of the same block, so it needs at most two blocks per CU -- fewer
   // blocks, fewer slabs for the finalize to read.
-  const int occ_cap = getenv("HCU_BW_OCC") ? std::max(1, atoi(getenv("HCU_BW_OCC"))) : 2;
+  const int occ_cap = 2;   // (grids for one block per CU measured +1 %)
   const int occ_kb = a.NPA ? std::min(a.occ, occ_cap) : a.occ;
   long kb = std::max(1L, (long)bw_cus() * occ_kb / per);
   kb = std::min(kb, total);

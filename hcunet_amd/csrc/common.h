@@ -599,7 +599,7 @@ struct WGradArgs {
   // wgrad8 (wgrad8.hip, v2 == 2): A image z-row stride (PA2 / PG2: plane
   // strides), MFMA form (0: 16x16x4, 1: 4x4x1 16-block), voxel blocks per
   // instruction and z taps on the column side (form 1)
-  int ARS, w8mode, w8nbv, w8nj, w8nh, w8dbg;
+  int ARS, w8mode, w8nbv, w8nj, w8nh;
   int w8off[128];                     // wgrad8 row (form 0) / row-quad (form 1) A image offsets
   // BatchNorm-backward apply of the gradient operand on load (wgrad8 form 0,
   // when the weight gradient is the apply's only consumer): G holds d(post-

@@ -252,11 +252,7 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b, int per
 
 int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n,
                     hipStream_t s) {
-  // HCU_PREP_PERM=0: the column-fastest vector order (A/B)
-  static const int perm = [] {
-    const char *e = getenv("HCU_PREP_PERM");
-    return !(e && e[0] == '0');
-  }();
+  const int perm = 1;   // the tap-fastest vector order (prep_perm; round 3: config 3 -8..-18 us)
   // HCU_PREP_TILED=1 (opt-in): the LDS-staged form where it applies; measured
   // 22 -> 33 us per config-2 step and equal on config 3, so the gather stays
   static const bool tiled = [] {

@@ -1018,9 +1018,9 @@ bool tails_enabled() {
   return on;
 }
 
-// rows x channels a finalize tail may read (HCU_BNB_TAIL_MAX, A/B)
+// rows x channels a finalize tail may read
 long tail_max_values() {
-  static const long v = getenv("HCU_BNB_TAIL_MAX") ? atol(getenv("HCU_BNB_TAIL_MAX")) : 4096;
+  static const long v = 4096;
   return v;
 }
 
@@ -1140,16 +1140,15 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 // gradient alone (the round-3 default) +7 us per config-2 step.
 bool ap_ok(const Ctx &c, const ConvLayer &L, bool with_dgrad) {
   static const int mode = getenv("HCU_AP") ? atoi(getenv("HCU_AP")) : 0;
-  static const bool bf_on = !(getenv("HCU_AP_BF16") && getenv("HCU_AP_BF16")[0] == '0');
-  // HCU_AP_MAX_MB: the largest dY (MB) applied on load.
-  static const double max_b = 1e6 * (getenv("HCU_AP_MAX_MB") ? atof(getenv("HCU_AP_MAX_MB")) : 8.0);
+  // the largest dY (bytes) applied on load
+  static const double max_b = 8e6;
   if (mode == 0 || c.p.is_chain || L.bn.index >= 64) return false;
   const WGradArgs &w = L.wg;
   const bool small = (double)L.out.vox() * L.out.Cs * L.out.es <= max_b;
   if (with_dgrad && (!small || !L.dgrad.use_bconv)) return false;
   // (the bf16 first layer's bwgrad with the operand apply ran 253 us against
   // 115 + 116 for bwgrad + the apply pass: only small bf16 layers)
-  if (w.use_bw) return bf_on && small && bwgrad_gap_ok(w);
+  if (w.use_bw) return small && bwgrad_gap_ok(w);
   if (w.v2 == 2) return w.w8mode == 0 && w.GCs <= 16 && (small || !with_dgrad);
   return w.v2 == 1 && small;
 }

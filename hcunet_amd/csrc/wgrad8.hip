@@ -74,7 +74,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   }
 
   lds_barrier();
-  if (a.w8dbg & 8) return;
   // ---- lane roles
   constexpr int NACC = NR;
   int aoff[NR];
@@ -150,13 +149,11 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   int ma = 0;                                        // valid A voxels: bit u*4 + j
   int mg = 0;                                        // GAP: valid G voxels: bit u*4 + j
 
-  const int dbg = a.w8dbg;   // HCU_W8_DBG (measurement only): 1 no MFMA, 2 no loads, 4 no LDS stores
   // Branch-free buffer loads straight into the prefetch registers (a load under
   // a branch is copied at the join, which waits for it): invalid positions read
   // an offset past the sample's buffer and return 0.
   constexpr int OOB = 0x7ffffff0;
   auto load = [&](int tt) {
-    if (dbg & 2) return;
     const int b = tt / ntiles;
     int tile = tt - b * ntiles;
     const int tyi = tile % KA(nty);
@@ -217,14 +214,13 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   };
 
   lds_barrier();
-  if (dbg & 32) return;
   if (t_beg < t_end) load(t_beg);
   for (int tt = t_beg; tt < t_end; ++tt) {
     lds_barrier();
     // ---- registers -> LDS (activation on A), transposed to z-major b128 stores
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      if (adst[u] < 0 || (dbg & 4)) continue;
+      if (adst[u] < 0) continue;
       const int cq = (tid + u * 256) % CA4;
       const floatx4 sc = *reinterpret_cast<const floatx4 *>(&actl[0][cq * 4]);
       const floatx4 sf = *reinterpret_cast<const floatx4 *>(&actl[1][cq * 4]);
@@ -244,7 +240,7 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      if (gdst[u] < 0 || (dbg & 4)) continue;
+      if (gdst[u] < 0) continue;
       if (GAP) {   // dy = dz*scale + (c1*y + c0), bn_bwd_apply's expression; 0 outside
         const int cq = (tid + u * 256) % CG4;
         const floatx4 gs = *reinterpret_cast<const floatx4 *>(&gapl[0][cq * 4]);
@@ -265,7 +261,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
     }
     lds_barrier();
     if (tt + 1 < t_end) load(tt + 1);                // lands while this tile computes
-    if (dbg & 1) continue;
     // K-steps of this wave (form 0: one tile column each, wave w takes w, w+4, ..;
     // form 1: NBv/4 columns each, wave w takes w/nh, w/nh + 4/nh, ..), software
     // pipelined: the next step's LDS reads are issued before this step's MFMAs
@@ -329,7 +324,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
     }
   }
 
-  if (dbg & 16) return;
   // ---- every wave stores its accumulators (b128, no serial rounds), then the
   // fixed-order sum over waves (and, form 1, over the voxel blocks)
   lds_barrier();
@@ -565,7 +559,6 @@ int plan_wgrad8(WGradArgs &a) {
     }
   }
   a.KB = (int)std::max(1L, best_kb);
-  a.w8dbg = getenv("HCU_W8_DBG") ? atoi(getenv("HCU_W8_DBG")) : 0;
   a.v2 = 2;
   return 0;
 }

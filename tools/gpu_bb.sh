@@ -27,5 +27,4 @@ run 4 4 f 2 12 12 12 64 128 3 3 2 0      # d4.c1 fwd
 HCU_BCONV_FORCE=32,2,4,0 run 4 2 f 4 254 254 15 32 32 3 3 1 1
 HCU_BCONV_FORCE=32,2,2 run 4 2 f 4 254 254 15 32 32 3 3 1 1
 HCU_BCONV_FORCE=32,1,4 run 4 2 f 4 254 254 15 32 32 3 3 1 1
-HCU_BCONV_LDS_KB=160 HCU_BCONV_FORCE=32,2,4 run 4 2 f 4 254 254 15 32 32 3 3 1 1
 tail -12 $O/${TAG}.txt
