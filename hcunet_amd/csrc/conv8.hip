@@ -384,7 +384,8 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
     const int HVP = round_up(HV, 16) + 8;
     const long lds = conv8_lds(a, C4, HVP, G);
     const long tiles = (long)a.B * cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz;
-    // <= 12 prefetched elements per thread (16 spills registers at G = 8)
+    // <= 12 prefetched elements per thread (16 spills registers at G = 8; 16
+    // at G <= 4, which lets d1.c1's input gradient take G = 4, measured equal)
     if (lds > 80 * 1024 || HV * C4 > 12 * 256) continue;
     a.G8 = G;
     a.TX = TX;
