@@ -658,9 +658,9 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   a.Mtot = a.taps_rows ? T * a.ACs + (a.bias_row ? 1 : 0) : a.ACs;
   a.Ntot = a.taps_rows ? a.GCs : T * a.GCs;
   // voxel tile: TX*TY = 32 (or 64 when the halo fits), TZ = the whole Z (<= 16)
-  // (TZ <= 8 -- half the image, two resident blocks, twice the slabs --
-  // measured 7.25 vs 6.63 ms per config-3 step)
-  const int ntz = cdiv(a.PZ, 16);
+  // (TZ <= 8 for every layer -- half the image, two resident blocks, twice
+  // the slabs -- measured 7.25 vs 6.63 ms per config-3 step)
+  int ntz = cdiv(a.PZ, 16);
   a.TZ = cdiv(a.PZ, ntz);
   a.PA2 = a.CKA + 8;
   a.PG2 = a.CKG + 8;
@@ -696,7 +696,23 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   }
   if (pick < -1) pick = -2 - pick;
   if (pick < 0) pick = t0i;
-  const long lds = set_tile(pick);
+  long lds = set_tile(pick);
+  // A layer whose full-Z tile leaves one block per CU and whose slab is small
+  // (the level-0/1 layers: the next tile's loads are exposed, the finalize
+  // reads little) takes half the Z extent per tile: two resident blocks
+  // Config 3 (interleaved A/B, 2 runs): slabs <= 64 KB (d0.c2, u3.c2) 6.50 vs
+  // 6.62 ms/step without; <= 160 KB 6.56; <= 640 KB 6.96.
+  if (lds > 80 * 1024 && (long)a.Mtot * a.Ntot * 4 <= 64 * 1024 && a.PZ > 8) {
+    ntz = cdiv(a.PZ, 8);
+    a.TZ = cdiv(a.PZ, ntz);
+    const int TZh = a.TZ;
+    a.HAZ = (TZh - 1) * a.asz + (a.taps_rows ? (a.KZ - 1) * a.adz : 0) + 1;
+    a.HGZ = (TZh - 1) * a.gsz + (a.taps_rows ? 0 : (a.KZ - 1) * a.gdz) + 1;
+    a.HAV = a.HAX * a.HAY * a.HAZ;
+    a.HGV = a.HGX * a.HGY * a.HGZ;
+    a.PTV = a.TX * a.TY * TZh;
+    lds = ((long)a.HAV * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
+  }
   if (lds > 160 * 1024) return fail(4, "bwgrad: tile does not fit LDS");
   a.lds_bytes = (int)((lds + 15) & ~15L);
   a.fHAZ = FastDiv(a.HAZ);
