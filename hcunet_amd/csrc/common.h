@@ -86,8 +86,9 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
 inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
-// CUs' worth of resident workgroups an fp32 weight-gradient launch (the
-// backward's branch stream) is sized for: 256 fills the chip; fewer leave
+// CUs' worth of resident workgroups the generic weight-gradient launch (the
+// backward's branch stream) is sized for (wgrad3 / wgrad2 / wgrad8 fix their
+// own: 192 / 192 / 256, measured per family): 256 fills the chip; fewer leave
 // slots for the chain stream's kernels to start while the branch runs and
 // write fewer slabs (HCU_SIDE_CUS, A/B).  Config 2, interleaved A/B (2 runs
 // each): 256 -> 2.164 ms/step, 240 -> 2.226, 224 -> 2.150, 192 -> 2.267,

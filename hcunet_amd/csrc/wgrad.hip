@@ -547,7 +547,9 @@ static int plan_wgrad2(WGradArgs &a, int target_blocks) {
   const long total = (long)a.B * a.ntx * a.nty * a.ntz;
   const long per = (long)a.mchunks * a.nchunks;
   a.occ = std::max(1, std::min(8, (int)(160 * 1024 / a.lds_bytes)));
-  long kb = std::max(1L, (long)side_cus() * a.occ / per);
+  // 192 CUs leaves room for the chain stream (config 2 A/B, 3 reps: 192 -> 2.038-2.051,
+  // 160 -> 2.060-2.067, 128 -> 2.063-2.081, 224 -> 2.070-2.082 ms/step).
+  long kb = std::max(1L, 192L * a.occ / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
   a.v2 = 1;

@@ -245,8 +245,8 @@ static int cm_stride(int n) { return n + ((2 - n % 32) + 32) % 32; }
 // fp32) for wgrad3_kernel; 0 when it applies.  Chooses the channel chunk, the
 // row subtiles per wave (3 / 5 / 9), the voxel tile and the number of voxel
 // blocks by a per-CU time model: MFMA cycles of a block + its staging (~32
-// bytes a cycle) + its slab write, the blocks spread over the CUs the branch
-// stream is sized for (side_cus).
+// bytes a cycle) + its slab write, the blocks spread over the 192 CUs the branch
+// stream is sized for.
 int plan_wgrad3(WGradArgs &a) {
   if (!wgrad3_enabled() || !a.taps_rows) return 1;
   const bool ph = a.nph > 1;   // ConvTranspose3d phase form: A padded, G strided by the phases
@@ -265,7 +265,10 @@ int plan_wgrad3(WGradArgs &a) {
   const int NS = cw % 64 == 0 ? 4 : 2;
   const int CKG = NS * 16;
   const int nco = ncols / CKG;
-  const int cus = side_cus();
+  // Grid sized for 192 CUs: the weight-gradient branch overlaps the chain stream
+  // (config 2 A/B, 3 reps: 192 -> 2.038-2.051, 176 -> 2.062-2.081, 208 -> 2.084-2.098,
+  // 160 -> 2.083-2.090, side_cus() 224 -> 2.113-2.126 ms/step).
+  const int cus = 192;
   const int mss[3] = {9, 5, 3};
   const int ckas[3] = {64, 32, 16};
   const int txys[4][2] = {{4, 4}, {4, 2}, {2, 4}, {2, 2}};

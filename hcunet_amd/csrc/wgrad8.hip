@@ -550,7 +550,10 @@ int plan_wgrad8(WGradArgs &a) {
   const long total = (long)a.B * a.ntx * a.nty * a.ntz;
   long best_kb = 1, best_cost = 1L << 62;
   for (int per_cu = 1; per_cu <= 2; ++per_cu) {
-    const long kb = std::min(total, (long)side_cus() * per_cu / nci);
+    // The whole chip: wgrad8 slabs run where the chain stream is thin (config 2 A/B,
+    // 3 reps: 256 CUs with wgrad3/wgrad2 at 192 -> 2.061-2.068 ms/step; side_cus() 224
+    // for all three -> 2.113-2.126).
+    const long kb = std::min(total, 256L * per_cu / nci);
     if (kb < 1) continue;
     const long cost = cdiv(total, kb) * per_cu;
     if (cost < best_cost || (cost == best_cost && kb > best_kb)) {
