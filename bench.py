@@ -124,6 +124,9 @@ def tagify(rocprof_name):
             return n.split('<', 1)[0]   # element-type-only templates: timed under the base name
     n = n.replace('<float,', '<f32,').replace('<unsignedshort,', '<bf16,')
     n = n.replace(',false>', '>').replace(',true>', ',bnb>')
+    if n.startswith('bconv_kernel<') and n.count(',') == 5:
+        # the fused-BatchNorm-backward flag is an int template argument there
+        n = re.sub(r',0>$', '>', re.sub(r',1>$', ',bnb>', n))
     return n
 
 

@@ -1467,20 +1467,42 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   tag(std::string("prep"), "fwd");
   // training forwards lay out the input-gradient weight images too; laying
   // them out on the backward's branch instead measured equal on config 3 and
-  // ~10 us slower on config 2
-  if (training && !p.prep_bwd.empty()) {
+  // ~10 us slower on config 2.  A split forward (hcu_unet_forward) lays out
+  // level 0's forward images on the chain and every other image on the
+  // branch, which the chain waits for only before level 1.
+  const size_t n0 = std::min<size_t>(2, p.prep_fwd.size());   // d0.c1, d0.c2 (job order)
+  hipEvent_t ev_rest = nullptr;
+  if (split && training) {
     if (int e = c.fork()) return e;
-    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
-                                (int)p.prep_bwd.size(), c.wstream()))
+    if (p.prep_fwd.size() > n0) {
+      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data() + n0,
+                                  (int)(p.prep_fwd.size() - n0), c.ws))
+        return e;
+      ev_rest = p.ev_fork_ring[p.fork_next++ % HCU_FORK_RING];
+      HCU_HIP(hipEventRecord(ev_rest, c.ws));
+    }
+    if (!p.prep_bwd.empty())
+      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
+                                  (int)p.prep_bwd.size(), c.ws))
+        return e;
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data(), (int)n0, c.s))
+      return e;
+  } else {
+    if (training && !p.prep_bwd.empty()) {
+      if (int e = c.fork()) return e;
+      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
+                                  (int)p.prep_bwd.size(), c.wstream()))
+        return e;
+    }
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data(),
+                                (int)p.prep_fwd.size(), c.s))
       return e;
   }
-  if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data(),
-                              (int)p.prep_fwd.size(), c.s))
-    return e;
   const float *src = xcl;
   const float *ssc = nullptr, *ssh = nullptr;
   for (int i = 0; i < p.L; ++i) {
     const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
+    if (i == 1 && ev_rest) HCU_HIP(hipStreamWaitEvent(c.s, ev_rest, 0));
     if (int e = conv_forward(c, c1, src, ssc, ssh, training)) return e;
     const BNCoef b1 = coef_at(c.sv, c1.bn);
     if (int e = conv_forward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, training)) return e;
@@ -1565,10 +1587,20 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   }
   // The input layout change runs ahead of the captured sequence, so a fresh
   // input tensor every step (a data loader) does not key a new graph.
-  // (the forward runs on the caller's stream alone: forking the input-gradient
-  // weight re-layout onto the branch measured 60-110 us slower per config-2
-  // step in round 3)
-  const bool split = false;
+  // Large parameter sets lay out their deeper weight images on the branch
+  // stream while level 0 runs (Ctx in enqueue_forward).  Interleaved A/B, 3
+  // runs: config 3 (11.6 M parameters) 6.418-6.434 vs 6.448-6.453 ms/step;
+  // config 2 (0.7 M, ~23 us of re-layout) 2.103-2.129 vs 2.058-2.071: there
+  // the branch's kernels slow level 0 more than the overlap returns.
+  const bool split = p.n_params >= (int64_t)4 << 20 && training && side_enabled() && !timing_on() &&
+                     p.prep_fwd.size() > 2;
+  std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
+  if (split) {
+    lk.lock();
+    int dev = 0;
+    HCU_HIP(hipGetDevice(&dev));
+    if (int e = ensure_side(p, dev)) return e;
+  }
   if (graphs_for(p, false) && !timing_on()) {
     tag(std::string("in"), "fwd");
     if (int e = launch_to_cl(t->x, reinterpret_cast<float *>((char *)t->saved + p.xcl_off), p.B, p.xin.C,
