@@ -737,7 +737,11 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // blocks, fewer slabs for the finalize to read.
   const int occ_cap = 2;   // (grids for one block per CU measured +1 %)
   const int occ_kb = a.NPA ? std::min(a.occ, occ_cap) : a.occ;
-  long kb = std::max(1L, (long)bw_cus() * occ_kb / per);
+  // the network's first layer (<= 8 input channels) runs last on the branch,
+  // after the chain has finished: its grid may take the whole chip
+  static const int cus0 = getenv("HCU_BW_CUS0") ? atoi(getenv("HCU_BW_CUS0")) : 0;
+  const int cus = (cus0 > 0 && a.ACs <= 8) ? std::min(256, cus0) : bw_cus();
+  long kb = std::max(1L, (long)cus * occ_kb / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
   a.use_bw = 1;

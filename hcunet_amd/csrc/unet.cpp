@@ -477,10 +477,23 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     w.taps_rows = 1;
     w.bias_row = phase_mode == 1 ? 1 : 0;
     w.nph = nph; w.phx = u.S[0]; w.phy = u.S[1]; w.phz = u.S[2]; w.GCout = o;
+    const WGradArgs w0 = w;
     if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == (phase_mode == 1 ? 1 : 3)) {
       u.wgp = w;
       u.wg_phase = true;
       max_part = std::max(max_part, wgrad_partial_floats(w));
+    } else if (phase_mode == 3) {
+      // (=3: where wgrad3 does not apply -- fewer than 32 output channels -- the
+      // phase form on wgrad2 with its bias row, instead of wgrad_kernel + chansum)
+      w = w0;
+      w.bias_row = 1;
+      if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == 1) {
+        u.wgp = w;
+        u.wg_phase = true;
+        max_part = std::max(max_part, wgrad_partial_floats(w));
+      } else {
+        set_error("");
+      }
     } else {
       set_error("");
     }

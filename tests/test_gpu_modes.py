@@ -211,3 +211,34 @@ def test_tiled_weight_relayout_matches_gather(tmp_path, bf16):
     bad = [(it, k, (x - y).abs().max().item())
            for it in range(3) for k, (x, y) in enumerate(zip(a[it], b[it])) if not torch.equal(x, y)]
     assert not bad, bad[:8]
+
+
+# Kernel-family switches: each selects another kernel family (or grid size,
+# or finalize schedule) for the same layers.  They exist for A/B runs and as
+# fallbacks; here every one is held to the default's results.
+FALLBACKS_F32 = [{'HCU_NO_CONV8': '1'}, {'HCU_NO_CONV2': '1'}, {'HCU_NO_BCONV_F32': '1'},
+                 {'HCU_NO_WGRAD8': '1'}, {'HCU_NO_WGRAD2': '1'}, {'HCU_NO_BNFUSE': '1'},
+                 {'HCU_WGF_DEFER': '0'}, {'HCU_SIDE_CUS': '128'}]
+FALLBACKS_BF16 = [{'HCU_BW_CUS': '128'}, {'HCU_BW_CUS0': '256'}, {'HCU_NO_BNFUSE': '1'},
+                  {'HCU_WGF_DEFER': '0'}]
+
+
+@pytest.mark.parametrize('bf16', ['0', '1'])
+def test_kernel_family_switches_match_default(tmp_path, bf16):
+    """Every kernel-family / grid / schedule switch gives the default's outputs
+    and gradients to reassociation of the same sums (fp32: 1e-4 of each
+    tensor's largest element; bf16: 2e-2, one bf16 rounding of a reassociated
+    operand; plus 1e-6 absolute for the BatchNorm-cancelled conv biases)."""
+    kw = KW if bf16 == '0' else KW.replace('[8, 16, 32, 64, 128]', '[16, 32, 64, 128]')
+    ref = _run(tmp_path, 'fbdef' + bf16, {'HCU_TEST_BF16': bf16}, kw=kw)
+    rel = 1e-4 if bf16 == '0' else 2e-2
+    bad = []
+    for i, sw in enumerate(FALLBACKS_F32 if bf16 == '0' else FALLBACKS_BF16):
+        got = _run(tmp_path, 'fb%d_%s' % (i, bf16), dict(sw, HCU_TEST_BF16=bf16), kw=kw)
+        for it in range(3):
+            for k, (a, b) in enumerate(zip(ref[it], got[it])):
+                tol = rel * a.abs().max().item() + 1e-6
+                d = (a - b).abs().max().item()
+                if not d <= tol:
+                    bad.append((sw, it, k, d, tol))
+    assert not bad, bad[:8]
