@@ -737,10 +737,10 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // blocks, fewer slabs for the finalize to read.
   const int occ_cap = 2;   // (grids for one block per CU measured +1 %)
   const int occ_kb = a.NPA ? std::min(a.occ, occ_cap) : a.occ;
-  // the network's first layer (<= 8 input channels) runs last on the branch,
-  // after the chain has finished: its grid may take the whole chip
-  static const int cus0 = getenv("HCU_BW_CUS0") ? atoi(getenv("HCU_BW_CUS0")) : 0;
-  const int cus = (cus0 > 0 && a.ACs <= 8) ? std::min(256, cus0) : bw_cus();
+  // The network's first layer (<= 8 input channels) runs last on the branch,
+  // after the chain has finished: its grid takes the whole chip (config 3,
+  // interleaved A/B, 3 runs: 6.433-6.449 vs 6.455-6.461 ms/step at 224 CUs).
+  const int cus = a.ACs <= 8 ? 256 : bw_cus();
   long kb = std::max(1L, (long)cus * occ_kb / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;

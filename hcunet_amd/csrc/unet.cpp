@@ -457,7 +457,10 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
   // finalize's serial bias sum over the phases is slow); HCU_CONVT_PHASE_WG=1:
   // on wgrad2 with the bias row (measured +13 us per config-2 step against
   // the per-tap wgrad_kernel + chansum: its wider slabs double the finalize
-  // reads), =0: off.
+  // reads), =0: off.  (The wgrad2 form only for u2.up / u3.up, where wgrad3
+  // does not apply -- fewer than 32 output channels: u2.up 30 -> 16 us and
+  // u3.up 30 -> 17 us with their chansums, and still 2.105-2.128 vs
+  // 2.059-2.072 ms per config-2 step, interleaved, 3 runs: their finalizes.)
   static const int phase_mode = getenv("HCU_CONVT_PHASE_WG") ? atoi(getenv("HCU_CONVT_PHASE_WG")) : 2;
   if (!bf && u.fused && o % 4 == 0 && phase_mode) {
     // dW'[(j, ci)][(q, co)] = sum_o A[o + j - (J-1)][ci] * dU[o*S + q][co] over the
@@ -477,23 +480,10 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     w.taps_rows = 1;
     w.bias_row = phase_mode == 1 ? 1 : 0;
     w.nph = nph; w.phx = u.S[0]; w.phy = u.S[1]; w.phz = u.S[2]; w.GCout = o;
-    const WGradArgs w0 = w;
     if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == (phase_mode == 1 ? 1 : 3)) {
       u.wgp = w;
       u.wg_phase = true;
       max_part = std::max(max_part, wgrad_partial_floats(w));
-    } else if (phase_mode == 3) {
-      // (=3: where wgrad3 does not apply -- fewer than 32 output channels -- the
-      // phase form on wgrad2 with its bias row, instead of wgrad_kernel + chansum)
-      w = w0;
-      w.bias_row = 1;
-      if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == 1) {
-        u.wgp = w;
-        u.wg_phase = true;
-        max_part = std::max(max_part, wgrad_partial_floats(w));
-      } else {
-        set_error("");
-      }
     } else {
       set_error("");
     }

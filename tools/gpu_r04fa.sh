@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# switch test + config-3 bench with the 256-CU first-layer weight gradient
+# switch test, then the measurement pass part a (GPU tests, config 2/3 profiles, PMC, SQ)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out; mkdir -p $O
@@ -7,5 +7,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_modes.py -q --timeout 500 -
   -k "kernel_family" > $O/fb_tests.log 2>&1
 rc=$?; tail -2 $O/fb_tests.log; grep -E '^E ' $O/fb_tests.log | cut -c1-1500 | head -4
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 300 python -u bench.py --config 3 --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing > $O/v3.json 2> $O/v3.err || { tail -20 $O/v3.err; exit 1; }
-cut -c1-200 $O/v3.json
+bash tools/gpu_final_a.sh r04 1
