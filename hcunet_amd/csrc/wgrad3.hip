@@ -36,7 +36,7 @@ bool wgrad3_enabled() {   // HCU_WGRAD3=0 keeps the deep layers on wgrad2 (A/B)
   return on;
 }
 
-constexpr int kW3Loads = 8;   // 16-byte staging loads in flight per thread
+constexpr int kW3Loads = 8;   // 16-byte staging loads in flight per thread (serial staging)
 
 template <int MS, int NS>
 __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
@@ -50,10 +50,19 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
   const bool bias_block = a.bias_row && tapc == 0 && cic == 0;
   const int HAZP = a.HAZP, HAYZ = a.HAY * a.HAZP, TZP = a.TZP;
   const int HAV = a.HAX * a.HAY * HAZP, PTP = a.TX * a.TY * TZP;
+  const int NK = PTP / 4;                            // K-steps of a tile (4 voxels each)
   float *alds = smem;                                // [CKA + 1][RSA]  (+ zero row)
   float *glds = alds + (size_t)(CKA + 1) * RSA;      // [CKG + 1][RSG]  (+ zero row)
+  int *hvtab = reinterpret_cast<int *>(glds + (size_t)(CKG + 1) * RSG);   // [NK] halo voxel of K-step k
+  float *dummy = reinterpret_cast<float *>(hvtab + NK);                   // [4][64] sink of the padding lanes
   for (int i = tid; i < RSA; i += 256) alds[(size_t)CKA * RSA + i] = 0.f;
   for (int i = tid; i < RSG; i += 256) glds[(size_t)CKG * RSG + i] = 0.f;
+  for (int k = tid; k < NK; k += 256) {
+    const int row = k / (TZP / 4), z0 = (k - row * (TZP / 4)) * 4;
+    int lx, ly;
+    a.fTY.divmod(row, lx, ly);
+    hvtab[k] = lx * HAYZ + ly * HAZP + z0;
+  }
 
   // this lane's operand bases: A row (tap, channel) of each of the wave's row
   // subtiles (tap offset in halo voxels folded in), G column of each column
@@ -68,13 +77,13 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
       const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
       off = c * RSA + kx * a.adx * HAYZ + ky * a.ady * HAZP + kz * a.adz;
     }
-    aoff[m] = off;
+    aoff[m] = off + kq;
   }
   int goff[NS];
 #pragma unroll
   for (int n = 0; n < NS; ++n) {
     const int c = n * 16 + r16;
-    goff[n] = (c < CKG && co0 + c < a.Ntot) ? c * RSG : CKG * RSG;
+    goff[n] = ((c < CKG && co0 + c < a.Ntot) ? c * RSG : CKG * RSG) + kq;
   }
   // ConvTranspose3d phase form (WGradArgs::nph): the block's columns lie in
   // one stride phase q; G is read at o*S + q, channel co0 - q*GCout
@@ -93,121 +102,156 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
     for (int n = 0; n < NS; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int n = 0; n < NS; ++n) accb[n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const bool do_bias = bias_block && wave == 0;
+  // wave-uniform (a scalar branch in the MFMA loop)
+  const bool do_bias = __builtin_amdgcn_readfirstlane((int)(bias_block && wave == 0)) != 0;
   const bool act = a.a_scale != nullptr;
-  const int CA4 = CKA / 4, CG4 = CKG / 4;
+  // channel groups per staged voxel: powers of two (plan_wgrad3), so the
+  // element -> (voxel, group) split is a shift; a thread always stages the
+  // same 4-channel group (256 % CA4 == 0, 256 % CG4 == 0)
+  const int lgA = __builtin_ctz(CKA / 4), lgG = __builtin_ctz(CKG / 4);
+  const int ca = ci0 + (tid & ((1 << lgA) - 1)) * 4, cg = gcb + (tid & ((1 << lgG) - 1)) * 4;
+  const int rowa = (tid & ((1 << lgA) - 1)) * 4 * RSA, rowg = (tid & ((1 << lgG) - 1)) * 4 * RSG;
+  const bool cok_a = ca < a.ACs, cok_g = cg < a.GCs && co0 + (tid & ((1 << lgG) - 1)) * 4 < a.Ntot;
+  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (act && cok_a) {
+    sc = *reinterpret_cast<const float4 *>(a.a_scale + ca);
+    sh = *reinterpret_cast<const float4 *>(a.a_shift + ca);
+  }
+  const int sampA = a.AX * a.AY * a.AZ * a.ACs, sampG = a.GX * a.GY * a.GZ * a.GCs;   // floats (< 2^29, plan)
+  const int nA = HAV << lgA, nG = PTP << lgG;
 
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
   const int KBt = (int)gridDim.x, kbi = (int)blockIdx.x;
   const int tpb = (total + KBt - 1) / KBt;
-  const int t_end = min(total, kbi * tpb + tpb);
-  for (int tt = kbi * tpb; tt < t_end; ++tt) {
-    const int b = tt / ntiles;
+  const int t_beg = kbi * tpb, t_end = min(total, t_beg + tpb);
+  auto tile_of = [&](int tt, int &b, int &px0, int &py0, int &pz0) {
+    b = tt / ntiles;
     int tile = tt - b * ntiles;
     const int tzi = tile % a.ntz;
     tile /= a.ntz;
     const int tyi = tile % a.nty, txi = tile / a.nty;
-    const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    px0 = txi * a.TX;
+    py0 = tyi * a.TY;
+    pz0 = tzi * a.TZ;
+  };
+  auto rsrc = [&](const float *base, int floats) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, floats * 4, 0x00020000);
+  };
+  // element idx of the A halo / G tile: byte offset in its sample (past the
+  // buffer when invalid -> 0) and validity
+  auto a_elem = [&](int idx, int px0, int py0, int pz0, bool &ok) {
+    const int v = idx >> lgA;
+    int q, hz, hx, hy;
+    a.fHAZ.divmod(v, q, hz);
+    a.fHAY.divmod(q, hx, hy);
+    const int gx = px0 + hx - a.apx, gy = py0 + hy - a.apy, gz = pz0 + hz - a.apz;
+    ok = idx < nA && cok_a && (unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY &&
+         (unsigned)gz < (unsigned)a.AZ;
+    return ok ? (((gx * a.AY + gy) * a.AZ + gz) * a.ACs + ca) * 4 : 0x7ffffff0;
+  };
+  auto g_elem = [&](int idx, int px0, int py0, int pz0) {
+    const int p = idx >> lgG;
+    int q, lz, lx, ly;
+    a.fTZ.divmod(p, q, lz);
+    a.fTY.divmod(q, lx, ly);
+    const int ox = px0 + lx, oy = py0 + ly, oz = pz0 + lz;
+    const int gx = ox * a.gsx + gq[0], gy = oy * a.gsy + gq[1], gz = oz * a.gsz + gq[2];
+    const bool ok = idx < nG && cok_g && lz < a.TZ && ox < a.PX && oy < a.PY && oz < a.PZ && gx < a.GX &&
+                    gy < a.GY && gz < a.GZ;
+    return ok ? (((gx * a.GY + gy) * a.GZ + gz) * a.GCs + cg) * 4 : 0x7ffffff0;
+  };
+  auto act4 = [&](floatx4 x, bool ok) {
+    if (act) {
+      x[0] = ok ? fmaxf(fmaf(x[0], sc.x, sh.x), 0.f) : 0.f;
+      x[1] = ok ? fmaxf(fmaf(x[1], sc.y, sh.y), 0.f) : 0.f;
+      x[2] = ok ? fmaxf(fmaf(x[2], sc.z, sh.z), 0.f) : 0.f;
+      x[3] = ok ? fmaxf(fmaf(x[3], sc.w, sh.w), 0.f) : 0.f;
+    }
+    return x;
+  };
+  auto put4 = [&](float *d, int st, const floatx4 &x) {
+    d[0] = x[0];
+    d[st] = x[1];
+    d[2 * st] = x[2];
+    d[3 * st] = x[3];
+  };
+  for (int tt = t_beg; tt < t_end; ++tt) {
+    int b, px0, py0, pz0;
+    tile_of(tt, b, px0, py0, pz0);
     lds_barrier();   // the previous tile's operand reads are done
-    // ---- A halo, channel-major (activation applied, 0 outside the input)
-    for (int base = tid; base < HAV * CA4; base += kW3Loads * 256) {
-      float4 val[kW3Loads];
-      int dst[kW3Loads];
+    // ---- A halo, channel-major (activation applied, 0 outside the input).
+    // Branch-free: every load of a round is issued before the first LDS write
+    // (an invalid element reads an offset past the buffer -> 0).
+    const __amdgpu_buffer_rsrc_t rA = rsrc(a.A + (size_t)b * sampA, sampA);
+    for (int base = tid; base < nA; base += kW3Loads * 256) {
+      floatx4 val[kW3Loads];
+      uint32_t okm = 0;
 #pragma unroll
       for (int u = 0; u < kW3Loads; ++u) {
-        const int idx = base + u * 256;
-        val[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[u] = -1;
-        if (idx < HAV * CA4) {
-          const int c4 = idx % CA4, v = idx / CA4;
-          int q, hz, hx, hy;
-          a.fHAZ.divmod(v, q, hz);
-          a.fHAY.divmod(q, hx, hy);
-          dst[u] = c4 * 4 * RSA + v;
-          const int gx = px0 + hx - a.apx, gy = py0 + hy - a.apy, gz = pz0 + hz - a.apz, c = ci0 + c4 * 4;
-          if ((unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY && (unsigned)gz < (unsigned)a.AZ &&
-              c < a.ACs) {
-            val[u] = *reinterpret_cast<const float4 *>(
-                a.A + ((((size_t)b * a.AX + gx) * a.AY + gy) * a.AZ + gz) * a.ACs + c);
-            if (act) {
-              const float4 sc = *reinterpret_cast<const float4 *>(a.a_scale + c);
-              const float4 sh = *reinterpret_cast<const float4 *>(a.a_shift + c);
-              val[u].x = fmaxf(fmaf(val[u].x, sc.x, sh.x), 0.f);
-              val[u].y = fmaxf(fmaf(val[u].y, sc.y, sh.y), 0.f);
-              val[u].z = fmaxf(fmaf(val[u].z, sc.z, sh.z), 0.f);
-              val[u].w = fmaxf(fmaf(val[u].w, sc.w, sh.w), 0.f);
-            }
-          }
-        }
+        bool ok;
+        const int off = a_elem(base + u * 256, px0, py0, pz0, ok);
+        val[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rA, off, 0, 0));
+        okm |= (uint32_t)ok << u;
       }
 #pragma unroll
       for (int u = 0; u < kW3Loads; ++u) {
-        if (dst[u] < 0) continue;
-        float *d = alds + dst[u];
-        d[0] = val[u].x;
-        d[RSA] = val[u].y;
-        d[2 * RSA] = val[u].z;
-        d[3 * RSA] = val[u].w;
+        const int idx = base + u * 256;
+        const bool in = idx < nA;
+        put4(in ? alds + rowa + (idx >> lgA) : dummy + lane, in ? RSA : 64, act4(val[u], (okm >> u) & 1u));
       }
     }
     // ---- G tile, channel-major, z rows of TZP (0 past the output grid)
-    for (int base = tid; base < PTP * CG4; base += kW3Loads * 256) {
-      float4 val[kW3Loads];
-      int dst[kW3Loads];
+    const __amdgpu_buffer_rsrc_t rG = rsrc(a.G + (size_t)b * sampG, sampG);
+    for (int base = tid; base < nG; base += kW3Loads * 256) {
+      floatx4 val[kW3Loads];
+#pragma unroll
+      for (int u = 0; u < kW3Loads; ++u)
+        val[u] = __builtin_bit_cast(floatx4,
+                                    __builtin_amdgcn_raw_buffer_load_b128(rG, g_elem(base + u * 256, px0, py0, pz0), 0, 0));
 #pragma unroll
       for (int u = 0; u < kW3Loads; ++u) {
         const int idx = base + u * 256;
-        val[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[u] = -1;
-        if (idx < PTP * CG4) {
-          const int c4 = idx % CG4, p = idx / CG4;
-          const int lz = p % TZP, q = p / TZP;
-          int lx, ly;
-          a.fTY.divmod(q, lx, ly);
-          dst[u] = c4 * 4 * RSG + p;
-          const int ox = px0 + lx, oy = py0 + ly, oz = pz0 + lz, c = gcb + c4 * 4;
-          const int gx = ox * a.gsx + gq[0], gy = oy * a.gsy + gq[1], gz = oz * a.gsz + gq[2];
-          if (lz < a.TZ && ox < a.PX && oy < a.PY && oz < a.PZ && gx < a.GX && gy < a.GY && gz < a.GZ &&
-              c < a.GCs && co0 + c4 * 4 < a.Ntot)
-            val[u] = *reinterpret_cast<const float4 *>(
-                a.G + ((((size_t)b * a.GX + gx) * a.GY + gy) * a.GZ + gz) * a.GCs + c);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kW3Loads; ++u) {
-        if (dst[u] < 0) continue;
-        float *d = glds + dst[u];
-        d[0] = val[u].x;
-        d[RSG] = val[u].y;
-        d[2 * RSG] = val[u].z;
-        d[3 * RSG] = val[u].w;
+        const bool in = idx < nG;
+        put4(in ? glds + rowg + (idx >> lgG) : dummy + lane, in ? RSG : 64, val[u]);
       }
     }
     lds_barrier();
-    // ---- MFMA over the tile's voxels, 4 per K-step: lane group kq takes voxel
-    // p0 + kq of a z row (halo voxel hv0 + z0 + kq)
-    for (int row = 0; row < a.TX * a.TY; ++row) {
-      int lx, ly;
-      a.fTY.divmod(row, lx, ly);
-      const int hv0 = lx * HAYZ + ly * HAZP + kq, p0 = row * TZP + kq;
-      for (int z0 = 0; z0 < TZP; z0 += 4) {
-        float bv[NS];
+    // ---- MFMA over the tile's voxels, 4 per K-step (lane group kq takes
+    // voxel 4k + kq of the tile, halo voxel hvtab[k] + kq); the operands of
+    // step k + 1 are read while the MFMAs of step k run
+    float av0[MS], bv0[NS], av1[MS], bv1[NS];
+    // (hv: the K-step's halo voxel, read from hvtab two steps ahead)
+    auto ld = [&](int k, int hv, float (&av)[MS], float (&bv)[NS]) {
+      const int kk = min(k, NK - 1);
 #pragma unroll
-        for (int n = 0; n < NS; ++n) bv[n] = glds[goff[n] + p0 + z0];
+      for (int n = 0; n < NS; ++n) bv[n] = glds[goff[n] + 4 * kk];
 #pragma unroll
-        for (int m = 0; m < MS; ++m) {
-          const float av = alds[aoff[m] + hv0 + z0];
+      for (int m = 0; m < MS; ++m) av[m] = alds[aoff[m] + hv];
+    };
+    auto mf = [&](const float (&av)[MS], const float (&bv)[NS]) {
 #pragma unroll
-          for (int n = 0; n < NS; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[n], acc[m][n], 0, 0, 0);
-        }
-        if (do_bias) {
+      for (int m = 0; m < MS; ++m)
 #pragma unroll
-          for (int n = 0; n < NS; ++n)
-            accb[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, bv[n], accb[n], 0, 0, 0);
-        }
+        for (int n = 0; n < NS; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int n = 0; n < NS; ++n) accb[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(1.f, bv[n], accb[n], 0, 0, 0);
       }
+    };
+    int hvA = hvtab[0], hvB = hvtab[min(1, NK - 1)];
+    ld(0, hvA, av0, bv0);
+    hvA = hvtab[min(2, NK - 1)];
+    for (int k = 0; k < NK; k += 2) {
+      ld(k + 1, hvB, av1, bv1);
+      hvB = hvtab[min(k + 3, NK - 1)];
+      __builtin_amdgcn_sched_barrier(0);
+      mf(av0, bv0);
+      ld(k + 2, hvA, av0, bv0);
+      hvA = hvtab[min(k + 4, NK - 1)];
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 1 < NK) mf(av1, bv1);
     }
   }
 
@@ -256,6 +300,9 @@ int plan_wgrad3(WGradArgs &a) {
   // (16-channel inputs stay on wgrad2: d2.c1 of config 2 ran 65 us here
   // against 52 us there; every wider layer measured faster here)
   if (a.ACs % 32 || a.g_y) return 1;
+  // 32-bit buffer offsets within one sample
+  if ((double)a.AX * a.AY * a.AZ * a.ACs >= (double)(1 << 29) || (double)a.GX * a.GY * a.GZ * a.GCs >= (double)(1 << 29))
+    return 1;
   const int T = a.KX * a.KY * a.KZ;
   const int ntz = cdiv(a.PZ, 16), TZ = cdiv(a.PZ, ntz), TZP = round_up(TZ, 4);
   const int HAZP = TZP + (a.KZ - 1) * a.adz;
@@ -292,7 +339,7 @@ int plan_wgrad3(WGradArgs &a) {
         const int HAX = TX + (a.KX - 1) * a.adx, HAY = TY + (a.KY - 1) * a.ady;
         const int HAV = HAX * HAY * HAZP, PTP = TX * TY * TZP;
         const int RSA = cm_stride(HAV), RSG = cm_stride(PTP);
-        const long lds = ((long)(CKA + 1) * RSA + (long)(CKG + 1) * RSG) * 4;
+        const long lds = ((long)(CKA + 1) * RSA + (long)(CKG + 1) * RSG + PTP / 4 + 256) * 4;
         if (lds > 150 * 1024) continue;
         // two resident blocks (LDS <= 80 KB) overlap one's staging with the
         // other's MFMAs; one block pays both
@@ -344,6 +391,7 @@ int plan_wgrad3(WGradArgs &a) {
           c.fHAZ = FastDiv(HAZP);
           c.fHAY = FastDiv(HAY);
           c.fTY = FastDiv(TY);
+          c.fTZ = FastDiv(TZP);   // G tile z rows (the staging's voxel decode)
           c.v2 = 3;
           bestA = c;
         }

@@ -24,6 +24,12 @@ SHAPES = {   # name: B, Cin, Cout, X, Y, Z, k
     'd0.c2': (2, 8, 8, 254, 254, 15, (3, 3, 1)),
     'd1.c1': (2, 8, 16, 127, 127, 14, (3, 3, 2)),
     'd1.c2': (2, 16, 16, 125, 125, 13, (3, 3, 1)),
+    'd2.c2': (2, 32, 32, 59, 59, 13, (3, 3, 1)),       # the deep fp32 levels (wgrad3)
+    'd3.c1': (2, 32, 64, 28, 28, 13, (3, 3, 2)),
+    'd3.c2': (2, 64, 64, 26, 26, 12, (3, 3, 1)),
+    'd4.c1': (2, 64, 128, 12, 12, 12, (3, 3, 2)),
+    'd4.c2': (2, 128, 128, 10, 10, 11, (3, 3, 1)),
+    'u1.c1': (2, 32, 32, 24, 24, 12, (3, 3, 2)),
 }
 
 
