@@ -136,35 +136,10 @@ __device__ __forceinline__ floatx4 bload4(float *, __amdgpu_buffer_rsrc_t r, int
   return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 0));
 }
 
-// dz*s + (c1*y + c0) of the 16 bytes v (dz) and yv (pre-BN y), VEC channels;
-// s, c1, c0: VEC floats in LDS -- bn_bwd_apply_vec_kernel's arithmetic
-// (pointwise.hip), so the staged operand has the bits that kernel stores.
-__device__ __forceinline__ uint4 bapply16(uint16_t *, uint4 v, uint4 yv, const float *s, const float *c1,
-                                          const float *c0) {
-  float d[8], y[8];
-  unpack8(v, d);
-  unpack8(yv, y);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) d[j] = fmaf(d[j], s[j], fmaf(c1[j], y[j], c0[j]));
-  return pack8(d);
-}
-__device__ __forceinline__ uint4 bapply16(float *, uint4 v, uint4 yv, const float *s, const float *c1,
-                                          const float *c0) {
-  const floatx4 d = __builtin_bit_cast(floatx4, v), y = __builtin_bit_cast(floatx4, yv);
-  floatx4 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = fmaf(d[j], s[j], fmaf(c1[j], y[j], c0[j]));
-  return __builtin_bit_cast(uint4, o);
-}
-
-// MODE bit 0 (BNB): the fused BatchNorm+ReLU backward epilogue (+ the
-// finalize in the last workgroup when a.bfin.counter is set); bit 1 (AP): the
-// input operand is dz with the BatchNorm backward applied on load (a.in_y).
+// MODE 1 (BNB): the fused BatchNorm+ReLU backward epilogue.
 template <class E, int CV, int NSUB, int MPW, int NPF, int MODE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((MODE & 2) && NSUB * MPW <= 8 ? 2 : 1)))
-bconv_kernel(const GConvArgs a) {
+__global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   constexpr bool BNB = (MODE & 1) != 0;
-  constexpr bool AP = (MODE & 2) != 0;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // launch constants for the tile loop, read through kuni (common.h): they are
   // live only in the phase that uses them, not for the whole kernel
@@ -195,8 +170,7 @@ bconv_kernel(const GConvArgs a) {
   int *rowoff = rowpk + MPW * 64;                                 // [MPW*64]
   // per-block coefficients (LDS, read in short phases): [5][NT] = bias, bn
   // scale/shift/mean/invstd per stored column; [4][NT] statistics pivots of
-  // each wave; input activation [2][ICs] = scale, shift (AP: [3][ICs] = scale,
-  // c1, c0)
+  // each wave; input activation [2][ICs] = scale, shift
   float *coefL = reinterpret_cast<float *>(rowoff + MPW * 64);
   float *pivL = coefL + 5 * NT;
   float *actL = pivL + 4 * NT;
@@ -323,7 +297,6 @@ bconv_kernel(const GConvArgs a) {
   }
   const bool act = a.in_scale != nullptr;
   uint4 pf[NPFR];
-  uint4 pyf[AP ? NPFR : 1];   // AP: the pre-BN y at the same positions
   uint32_t okbits = 0;
   // halo of (tile, chunk) -> pf (branch-free: the validity of each element is
   // a mask, invalid elements read offset 0x7ffffff0, outside the buffer -> 0)
@@ -336,9 +309,6 @@ bconv_kernel(const GConvArgs a) {
     const char *bp = reinterpret_cast<const char *>(KA(in)) + (size_t)b * IX * bX;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, IX * (int)bX, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        AP ? (void *)(reinterpret_cast<const char *>(KA(in_y)) + (size_t)b * IX * bX) : (void *)bp, 0,
-        IX * (int)bX, 0x00020000);
     const int base_off = gx0 * (int)bX + gy0 * (int)bY + gz0 * (int)bZ + (chunk * CK + cv * VEC) * ES;
     okbits = 0;
 #pragma unroll
@@ -351,7 +321,6 @@ bconv_kernel(const GConvArgs a) {
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      if constexpr (AP) pyf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
   };
@@ -371,9 +340,6 @@ bconv_kernel(const GConvArgs a) {
     const char *bp = reinterpret_cast<const char *>(a.in) + (size_t)b * IX * bX;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, IX * (int)bX, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        AP ? (void *)(reinterpret_cast<const char *>(a.in_y) + (size_t)b * IX * bX) : (void *)bp, 0,
-        IX * (int)bX, 0x00020000);
     const int base_off = gx0 * (int)bX + gy0 * (int)bY + gz0 * (int)bZ + (chunk * CK + cv * VEC) * ES;
     okbits = 0;
 #pragma unroll
@@ -386,7 +352,6 @@ bconv_kernel(const GConvArgs a) {
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      if constexpr (AP) pyf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
   };
@@ -404,18 +369,12 @@ bconv_kernel(const GConvArgs a) {
       for (int c = tid; c < a.ICs; c += 256) {
         actL[c] = a.in_scale[c];
         actL[a.ICs + c] = a.in_shift[c];
-        if (AP) actL[2 * a.ICs + c] = a.in_c0[c];
       }
   };
-  // BatchNorm+ReLU of VEC channels (AP: the BatchNorm backward of dz), 0
-  // outside the input
-  auto activate = [&](uint4 v, uint4 yv, bool ok, int chunk) -> uint4 {
+  // BatchNorm+ReLU of VEC channels, 0 outside the input
+  auto activate = [&](uint4 v, bool ok, int chunk) -> uint4 {
     if (!ok) return make_uint4(0u, 0u, 0u, 0u);
     const int c = chunk * CK + cv * VEC;
-    if constexpr (AP) {
-      const int ICs = KA(ICs);
-      return bapply16(tag, v, yv, actL + c, actL + ICs + c, actL + 2 * ICs + c);
-    }
     if (!act) return v;
     return bact16(tag, v, actL + c, actL + KA(ICs) + c);
   };
@@ -428,11 +387,8 @@ bconv_kernel(const GConvArgs a) {
     const char *bp = reinterpret_cast<const char *>(a.in) + (size_t)b * a.IX * bX;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, a.IX * (int)bX, 0x00020000);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        AP ? (void *)(reinterpret_cast<const char *>(a.in_y) + (size_t)b * a.IX * bX) : (void *)bp, 0,
-        a.IX * (int)bX, 0x00020000);
     for (int base = tid / CV; base < HV; base += 4 * VS) {
-      uint4 val[4], yval[AP ? 4 : 1];
+      uint4 val[4];
       bool okv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -446,7 +402,6 @@ bconv_kernel(const GConvArgs a) {
         const int off = ok ? gx * (int)bX + gy * (int)bY + gz * (int)bZ + (chunk * CK + cv * VEC) * ES
                            : 0x7ffffff0;
         val[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        if constexpr (AP) yval[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
         okv[u] = ok;
       }
 #pragma unroll
@@ -454,7 +409,7 @@ bconv_kernel(const GConvArgs a) {
         const int v = base + u * VS;
         if (v < HV)
           *reinterpret_cast<uint4 *>(alds + v * CKP + cv * VEC) =
-              activate(val[u], yval[AP ? u : 0], okv[u], chunk);
+              activate(val[u], okv[u], chunk);
       }
     }
   };
@@ -638,7 +593,7 @@ bconv_kernel(const GConvArgs a) {
 #pragma unroll
         for (int u = 0; u < NPFR; ++u)   // every element is written (the waits stay exact)
           *reinterpret_cast<uint4 *>(alds + (hpk[u] >= 0 ? (tid / CV + u * VS) * CKP + cv * VEC : HV * CKP)) =
-              activate(pf[u], pyf[AP ? u : 0], (okbits >> u) & 1u, chunk);
+              activate(pf[u], (okbits >> u) & 1u, chunk);
         PH_MARK(0);
         if (wpre)
           wstore();
@@ -774,32 +729,14 @@ bconv_kernel(const GConvArgs a) {
       nn += e[2];
     }
     const size_t c = (size_t)blockIdx.x * a.CoutW + n0 + col;
-    if (fwdstat && a.fin.counter)
-      st_sc1_f4(a.stats + c * 4, make_float4(S1, S2, K, nn));   // handed to the last workgroup
-    else if (fwdstat)
+    if (fwdstat)
       *reinterpret_cast<float4 *>(a.stats + c * 4) = make_float4(S1, S2, K, nn);
-    else if (BNB && a.bfin.counter)
-      st_sc1_f2(a.stats + c * 2, make_float2(S1, S2));          // handed to the last workgroup
     else
       *reinterpret_cast<float2 *>(a.stats + c * 2) = make_float2(S1, S2);
   }
 #ifdef HCU_BCONV_PHASES
   ph_post[2] = (long long)__builtin_readcyclecounter();
 #endif
-  if (fwdstat && a.fin.counter) {   // fused BatchNorm finalize (BnFin, common.h)
-    if (bn_fin_ticket(a.fin.counter, reinterpret_cast<int *>(smem))) {
-      bn_fwd_finalize_tail(a.stats, a.fin, reinterpret_cast<double *>(smem));
-      if (tid == 0) bn_fin_reset(a.fin.counter);
-    }
-  }
-  if (BNB && a.bfin.counter) {   // BatchNorm-backward finalize of this column group (BnbFin)
-    int *flag = reinterpret_cast<int *>(smem) + 1024 + 32;
-    if (bn_ticket_n(a.bfin.counter + blockIdx.y, gridDim.x, flag)) {
-      bnb_finalize_tail(a.stats, gridDim.x, a.CoutW, n0, min(NT, a.OCs - n0), a.bn_scale, a.bn_invstd,
-                        a.bn_mean, a.bfin, reinterpret_cast<double *>(smem));
-      if (tid == 0) bn_fin_reset(a.bfin.counter + blockIdx.y);
-    }
-  }
 #ifdef HCU_BCONV_PHASES
   ph_flush();
 #endif
@@ -911,32 +848,11 @@ __global__ void __launch_bounds__(256) bconv_reduce_kernel(const GConvArgs a, in
         tn += red[q][2];
       }
       const int c = tid * GV + k;
-      if (fwdstat && a.fin.counter)
-        st_sc1_f4(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 4, make_float4(t1, t2, piv[k], tn));
-      else if (fwdstat)
+      if (fwdstat)
         *reinterpret_cast<float4 *>(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 4) =
             make_float4(t1, t2, piv[k], tn);
-      else if (a.bfin.counter)
-        st_sc1_f2(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 2, make_float2(t1, t2));
       else
         *reinterpret_cast<float2 *>(a.stats + ((size_t)blockIdx.x * a.CoutW + c) * 2) = make_float2(t1, t2);
-    }
-  }
-  if (a.bn_y && a.bfin.counter) {   // BatchNorm-backward finalize (BnbFin, common.h)
-    __shared__ double bred[512];
-    __shared__ int bflag;
-    if (bn_ticket_n(a.bfin.counter, gridDim.x, &bflag)) {
-      bnb_finalize_tail(a.stats, gridDim.x, a.CoutW, 0, a.OCs, a.bn_scale, a.bn_invstd, a.bn_mean, a.bfin,
-                        bred);
-      if (tid == 0) bn_fin_reset(a.bfin.counter);
-    }
-  }
-  if (fwdstat && a.fin.counter) {   // fused BatchNorm finalize (BnFin, common.h)
-    __shared__ double fred[768];
-    __shared__ int fflag;
-    if (bn_fin_ticket(a.fin.counter, &fflag)) {
-      bn_fwd_finalize_tail(a.stats, a.fin, fred);
-      if (tid == 0) bn_fin_reset(a.fin.counter);
     }
   }
 }
@@ -959,8 +875,6 @@ int launch_bconv_f32(const GConvArgs &a, hipStream_t s);
     switch (mode) {                                                                                  \
       BCONV_MODE(E_, TAG_, CV_, NS_, MP_, PF_, 0, "")                                                \
       BCONV_MODE(E_, TAG_, CV_, NS_, MP_, PF_, 1, ",bnb")                                            \
-      BCONV_MODE(E_, TAG_, CV_, NS_, MP_, PF_, 2, ",ap")                                             \
-      BCONV_MODE(E_, TAG_, CV_, NS_, MP_, PF_, 3, ",ap,bnb")                                         \
     }                                                                                                \
     launched = true;                                                                                 \
   }
@@ -984,7 +898,7 @@ template <> bool bconv_launch_cv<uint16_t, 1>(const GConvArgs &, hipStream_t, co
 template <> bool bconv_launch_cv<uint16_t, 2>(const GConvArgs &, hipStream_t, const dim3 &, double, double);
 template <> bool bconv_launch_cv<uint16_t, 4>(const GConvArgs &, hipStream_t, const dim3 &, double, double);
 #define BCONV_CV_BODY(E_, TAG_, CV_)                                                                 \
-  const int mode = (a.bn_y ? 1 : 0) | (a.in_y ? 2 : 0);                                              \
+  const int mode = a.bn_y ? 1 : 0;                                                                   \
   bool launched = false;                                                                             \
   BCONV_NS(E_, TAG_, CV_)                                                                            \
   return launched;
@@ -994,7 +908,6 @@ template <> bool bconv_launch_cv<uint16_t, 4>(const GConvArgs &, hipStream_t, co
   const dim3 grid(a.gridx, a.CoutW / (a.NSUB * 16), a.ksplit);                                       \
   if (grid.y > 65535 || grid.z > 65535) return fail(4, "bconv: grid too large");                     \
   if (a.ksplit > 1 && !a.partial) return fail(5, "bconv: K split needs a partial workspace");        \
-  if (a.in_y && !(a.in_scale && a.in_shift && a.in_c0)) return fail(5, "bconv: operand apply needs coefficients"); \
   const double fl = a.flops > 0 ? a.flops                                                            \
                                 : 2.0 * a.B * a.OX * a.OY * a.OZ * (double)a.Cout * a.nph * a.KX *   \
                                       a.KY * a.KZ * a.ICs;                                           \

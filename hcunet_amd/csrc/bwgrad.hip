@@ -305,9 +305,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
 // in flight while the current tile's MFMAs run, and a tile costs two LDS-only
 // barriers.  The halo coordinates of every register slot are tile-independent
 // and decoded once.
-// GAP: the gradient operand is BatchNorm-backward applied on load (WGradArgs::g_y):
-// dz*scale + (c1*y + c0) in fp32, rounded to bf16 -- the bits bn_bwd_apply stores.
-template <int MSW, int NS, int NP, bool GAP>
+template <int MSW, int NS, int NP>
 __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -417,18 +415,8 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
   }
   const uint16_t *Ab = reinterpret_cast<const uint16_t *>(a.A);
   const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
-  const uint16_t *Yb = reinterpret_cast<const uint16_t *>(a.g_y);
   uint4 ra[NP], rg[NP];
-  constexpr int NPY = GAP ? NP : 1;
-  uint4 ry[NPY];
-  unsigned oka = 0, okg = 0;
-  float gsc[8], gc1[8], gc0[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    gsc[k] = GAP ? a.g_scale[co0 + cg * 8 + k] : 0.f;
-    gc1[k] = GAP ? a.g_c1[co0 + cg * 8 + k] : 0.f;
-    gc0[k] = GAP ? a.g_c0[co0 + cg * 8 + k] : 0.f;
-  }
+  unsigned oka = 0;
 
   auto load = [&](int tt) {
     const int b = tt / ntiles;
@@ -456,7 +444,6 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
       const int gx0 = px0 * a.gsx - a.gpx, gy0 = py0 * a.gsy - a.gpy, gz0 = pz0 * a.gsz - a.gpz;
       const size_t boff = (size_t)b * a.GX * a.GY * a.GZ * a.GCs + co0 + cg * 8;
       const uint16_t *base = Gb + boff;
-      okg = 0;
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
         const int h = hoG[k];
@@ -468,11 +455,6 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
         const size_t vo = (((size_t)gx * a.GY + gy) * a.GZ + gz) * a.GCs;
         rg[k] = make_uint4(0u, 0u, 0u, 0u);
         if (ok) rg[k] = *reinterpret_cast<const uint4 *>(base + vo);
-        if (GAP) {
-          ry[k % NPY] = make_uint4(0u, 0u, 0u, 0u);
-          if (ok) ry[k % NPY] = *reinterpret_cast<const uint4 *>(Yb + boff + vo);
-          okg |= (ok ? 1u : 0u) << k;
-        }
       }
     }
   };
@@ -493,15 +475,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
 #pragma unroll
     for (int k = 0; k < NP; ++k) {
       if (hoG[k] < 0) continue;
-      uint4 w = rg[k];
-      if (GAP && ((okg >> k) & 1u)) {
-        float d[8], yy[8];
-        unpack8(w, d);
-        unpack8(ry[k % NPY], yy);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = fmaf(d[j], gsc[j], fmaf(gc1[j], yy[j], gc0[j]));
-        w = pack8(d);
-      }
+      const uint4 w = rg[k];
       *reinterpret_cast<uint4 *>(glds + (size_t)(vg0 + k * vsG) * RSG + cg * 8) = w;
     }
   };
@@ -756,12 +730,6 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   return 0;
 }
 
-// The tilings with an operand-apply (GAP) instance: pipelined, MSW <= 3, NSB <= 4,
-// NP 8 or 16 (launch_bwgrad).
-bool bwgrad_gap_ok(const WGradArgs &a) {
-  return a.use_bw && (a.NPA == 8 || a.NPA == 16) && (a.MSW == 1 || a.MSW == 3) && a.NSB <= 4;
-}
-
 int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
   const dim3 grid(a.KB, a.mchunks, a.nchunks);
   const int T = a.KX * a.KY * a.KZ;
@@ -770,25 +738,13 @@ int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
   const double by = 2.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
                            (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
   bool ok = false;
-  if (a.g_y && !bwgrad_gap_ok(a)) return fail(4, "bwgrad: operand apply unsupported for this tiling");
 #define BWP(MS_, NS_, NP_)                                                                  \
-  if (!ok && a.NPA == NP_ && !a.g_y) {                                                      \
+  if (!ok && a.NPA == NP_) {                                                                \
     HCU_TIMED(s, "bwgrad_pipe_kernel<" #MS_ "," #NS_ "," #NP_ ">", fl, by,                    \
-              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_, false>), grid, dim3(256),  \
+              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_>), grid, dim3(256),         \
                                  a.lds_bytes, s, a));                                       \
     ok = true;                                                                              \
   }
-#define BWPG(MS_, NS_, NP_)                                                                 \
-  if (!ok && a.NPA == NP_ && a.g_y && a.MSW == MS_ && a.NSB <= NS_) {                       \
-    HCU_TIMED(s, "bwgrad_pipe_kernel<" #MS_ "," #NS_ "," #NP_ ",gap>", fl, by,                \
-              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_, true>), grid, dim3(256),   \
-                                 a.lds_bytes, s, a));                                       \
-    ok = true;                                                                              \
-  }
-  // operand-apply instances: the first layers' tilings (bwgrad_gap_ok)
-  BWPG(1, 1, 8) BWPG(1, 2, 8) BWPG(1, 4, 8) BWPG(3, 1, 8) BWPG(3, 2, 8) BWPG(3, 4, 8)
-  BWPG(1, 1, 16) BWPG(1, 2, 16) BWPG(1, 4, 16) BWPG(3, 1, 16) BWPG(3, 2, 16) BWPG(3, 4, 16)
-#undef BWPG
 #define BW(MS_, NS_)                                                                        \
   if (!ok && a.MSW == MS_ && a.NSB <= NS_) {                                                \
     BWP(MS_, NS_, 8) BWP(MS_, NS_, 16) BWP(MS_, NS_, 32)                                    \

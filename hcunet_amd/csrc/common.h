@@ -188,48 +188,9 @@ int fail(int code, const std::string &msg);
 struct BNCoef {
   float *scale, *shift, *mean, *invstd, *c1, *c0;  // [Cs] each
 };
-// Forward BatchNorm finalize fused into the producing convolution (training):
-// every workgroup writes its statistics row, then takes a ticket from
-// `counter`; the workgroup holding the last ticket combines all R rows in
-// fp64 (bn_fwd_finalize_tail) into the layer's coefficients and running
-// statistics, and resets the counter to 0.  counter == nullptr: not fused.
-struct BnFin {
-  const float *gamma, *beta;
-  float *rm, *rv;
-  const int64_t *nbt;
-  BNCoef coef;
-  double count;
-  float eps, momentum;
-  int C, Cs, R, W;
-  unsigned *counter;
-};
-// BatchNorm-backward finalize in the last workgroup of a kernel that writes
-// the (sum dz, sum dz*xhat) rows (the fused dgrad epilogue, the pool / dense
-// reductions, the out_conv backward): per column group g (the workgroups
-// sharing blockIdx.y) the workgroup taking the last ticket of counter[g]
-// sums the group's rows in fp64 in a fixed order and writes dbeta / dgamma
-// and the c1 / c0 coefficients of dy = dz*scale + c1*y + c0 (bn_bwd_finalize's
-// arithmetic), then resets counter[g] to 0.  counter == nullptr: no tail (the
-// separate bn_bwd_finalize launch).  The counters are zeroed once per call
-// (Ctx::counters) and the rows stored write-through (sc1).
-struct BnbFin {
-  float *dgamma, *dbeta;   // parameter gradients (nullable)
-  float *c1, *c0;          // [Cs] coefficients written
-  double count;            // elements per channel
-  int C;                   // real channels (c >= C get c1 = c0 = 0)
-  int training, accumulate;
-  unsigned *counter;       // [column groups] tickets
-};
 struct GConvArgs {
   const float *in;
   const float *in_scale, *in_shift;   // [ICs] or null
-  // Input gradient with the BatchNorm backward applied on load (AP instances,
-  // in_y != null): `in` holds dz of a BatchNorm layer whose pre-BN output is
-  // in_y (same layout), and the staged operand is dz*in_scale + (in_shift*y +
-  // in_c0) per channel (in_scale = BN scale, in_shift = c1, in_c0 = c0): the
-  // bits bn_bwd_apply would have stored.
-  const float *in_y, *in_c0;
-  BnbFin bfin;                        // BNB epilogue: finalize in the last workgroup
   const float *w;                     // [T][ICs][CoutW]
   const float *bias;                  // [Cout] or null
   float *out;
@@ -273,219 +234,8 @@ struct GConvArgs {
   // (channels-last activations, packed weights); partial stays fp32.
   int use_bconv;
   int bes;   // bconv element bytes: 2 (bf16 activations) or 4 (fp32); 0 = 2
-  BnFin fin;   // bconv forward with statistics: fused BatchNorm finalize
 };
 
-// The last-workgroup BatchNorm forward finalize (256 threads, `red` = 768
-// doubles of LDS).  One pass over the R statistics rows: TPC threads per
-// channel each merge a strided subset of rows by the parallel-variance
-// (Chan) update of (n, mean, M2), loads issued 8 rows at a time; the TPC
-// partial states are then merged in a fixed tree order.  fp64 throughout,
-// deterministic (same rows, same order every run).
-__device__ __forceinline__ void chan_merge(double &n, double &mu, double &m2, double nb, double mub,
-                                           double m2b) {
-  if (nb <= 0.0) return;
-  if (n <= 0.0) {
-    n = nb; mu = mub; m2 = m2b;
-    return;
-  }
-  const double nn = n + nb, d = mub - mu;
-  mu += d * (nb / nn);
-  m2 += m2b + d * d * (n * nb / nn);
-  n = nn;
-}
-__device__ __forceinline__ void bn_fwd_finalize_tail(const float *stats, const BnFin &f, double *red) {
-  const int tid = threadIdx.x;
-  int TPC = 1;
-  while (TPC * 2 * f.C <= 256 && TPC < 64) TPC *= 2;
-  const int CPP = 256 / TPC, sub = tid % TPC;
-  for (int c0 = 0; c0 < f.Cs; c0 += CPP) {
-    const int c = c0 + tid / TPC;
-    double n = 0.0, mu = 0.0, m2 = 0.0;
-    if (c < f.C) {
-      for (int r0 = sub; r0 < f.R; r0 += 8 * TPC) {
-        float4 row[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int r = r0 + u * TPC;
-          row[u] = r < f.R ? *reinterpret_cast<const float4 *>(stats + ((size_t)r * f.W + c) * 4)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          if (row[u].w > 0.f) {   // row: sums of (y - K), (y - K)^2 over n = w values
-            const double nr = row[u].w, s1 = row[u].x;
-            chan_merge(n, mu, m2, nr, (double)row[u].z + s1 / nr, (double)row[u].y - s1 * s1 / nr);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    red[tid] = n;
-    red[256 + tid] = mu;
-    red[512 + tid] = m2;
-    __syncthreads();
-    for (int off = TPC / 2; off > 0; off >>= 1) {
-      if (sub < off) {
-        double a = red[tid], b = red[256 + tid], q = red[512 + tid];
-        chan_merge(a, b, q, red[tid + off], red[256 + tid + off], red[512 + tid + off]);
-        red[tid] = a;
-        red[256 + tid] = b;
-        red[512 + tid] = q;
-      }
-      __syncthreads();
-    }
-    if (sub == 0 && c < f.Cs) {
-      if (c >= f.C) {
-        f.coef.scale[c] = f.coef.shift[c] = f.coef.mean[c] = f.coef.invstd[c] = 0.f;
-        f.coef.c1[c] = f.coef.c0[c] = 0.f;
-      } else {
-        const double m = red[256 + tid];
-        double v = red[512 + tid] / red[tid];
-        if (v < 0.0) v = 0.0;
-        const float mean = (float)m, invstd = (float)(1.0 / sqrt(v + (double)f.eps));
-        if (f.rm) {
-          const double fm = f.momentum >= 0.f ? (double)f.momentum : 1.0 / (double)(f.nbt[0] + 1);
-          const double unb = f.count > 1.0 ? v * f.count / (f.count - 1.0) : v;
-          f.rm[c] = (float)(fm * m + (1.0 - fm) * (double)f.rm[c]);
-          f.rv[c] = (float)(fm * unb + (1.0 - fm) * (double)f.rv[c]);
-        }
-        const float g = f.gamma ? f.gamma[c] : 1.f, bb = f.beta ? f.beta[c] : 0.f;
-        const float sc = g * invstd;
-        f.coef.scale[c] = sc;
-        f.coef.shift[c] = bb - mean * sc;
-        f.coef.mean[c] = mean;
-        f.coef.invstd[c] = invstd;
-      }
-    }
-  }
-}
-
-// Hand-off of the statistics rows to the last workgroup without an L2
-// write-back (cdna_hip_programming.md §6 Guideline 16, sc1 form): the rows are
-// stored write-through (agent-scope atomic 8-byte stores = sc1), every wave
-// drains its stores, then one lane takes a ticket (relaxed agent fetch_add);
-// the workgroup with the last ticket acquires (one lane) and reads the rows
-// with plain loads.  (A release fence per workgroup writes back its XCD's
-// whole L2 under the still-running workgroups: measured +35..60 us a layer.)
-typedef __attribute__((address_space(1))) unsigned long long hcu_gu64;
-typedef __attribute__((address_space(1))) unsigned hcu_gu32;
-__device__ __forceinline__ void st_sc1_f4(float *p, float4 v) {
-  const unsigned long long lo = ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
-  const unsigned long long hi = ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z);
-  __hip_atomic_store((hcu_gu64 *)p, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((hcu_gu64 *)p + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Ticket of a workgroup whose waves have stored their rows with st_sc1_f4;
-// true (after the acquire) for the last workgroup.  flag_lds: one int of LDS.
-__device__ __forceinline__ bool bn_fin_ticket(unsigned *counter, int *flag_lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-    const unsigned t = __hip_atomic_fetch_add((hcu_gu32 *)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag_lds = t == nb - 1 ? 1 : 0;
-  }
-  __syncthreads();
-  const bool last = *(volatile int *)flag_lds != 0;
-  __syncthreads();
-  if (last) {
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
-  return last;
-}
-__device__ __forceinline__ void bn_fin_reset(unsigned *counter) {
-  __hip_atomic_store((hcu_gu32 *)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// The same hand-off for the workgroups of one column group: nb tickets on
-// `counter` (BnbFin).  The rows must have been stored with st_sc1_f2.
-__device__ __forceinline__ bool bn_ticket_n(unsigned *counter, unsigned nb, int *flag_lds) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add((hcu_gu32 *)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag_lds = t == nb - 1 ? 1 : 0;
-  }
-  __syncthreads();
-  const bool last = *(volatile int *)flag_lds != 0;
-  __syncthreads();
-  if (last) {
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
-  return last;
-}
-__device__ __forceinline__ void st_sc1_f2(float *p, float2 v) {
-  const unsigned long long u = ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
-  __hip_atomic_store((hcu_gu64 *)p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// BatchNorm-backward finalize of channels cb .. cb+nc-1 from the R rows
-// [R][W][2] (sum dz, sum dz*xhat), by the workgroup that took the last ticket
-// (BnbFin).  TPC threads per channel sum strided rows in fp64 (eight loads in
-// flight), then a fixed-order tree: deterministic.  red: 512 doubles of LDS.
-// c1 / c0 are bn_bwd_finalize_kernel's (pointwise.hip) arithmetic.
-__device__ __forceinline__ void bnb_finalize_tail(const float *rows, int R, int W, int cb, int nc,
-                                                  const float *scale, const float *invstd,
-                                                  const float *mean, const BnbFin &f, double *red) {
-  const int tid = threadIdx.x;
-  int TPC = 1;
-  while (TPC * 2 * nc <= 256 && TPC < 64) TPC *= 2;
-  const int CPP = 256 / TPC, sub = tid % TPC;
-  for (int g0 = 0; g0 < nc; g0 += CPP) {
-    const int j = g0 + tid / TPC, c = cb + j;
-    double s1 = 0.0, s2 = 0.0;
-    if (j < nc) {
-      for (int r0 = sub; r0 < R; r0 += 8 * TPC) {
-        float2 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int r = r0 + u * TPC;
-          v[u] = r < R ? *reinterpret_cast<const float2 *>(rows + ((size_t)r * W + c) * 2)
-                       : make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          s1 += (double)v[u].x;
-          s2 += (double)v[u].y;
-        }
-      }
-    }
-    __syncthreads();
-    red[tid] = s1;
-    red[256 + tid] = s2;
-    __syncthreads();
-    for (int off = TPC / 2; off > 0; off >>= 1) {
-      if (sub < off) {
-        red[tid] += red[tid + off];
-        red[256 + tid] += red[256 + tid + off];
-      }
-      __syncthreads();
-    }
-    if (sub == 0 && j < nc) {
-      const double db = red[tid], dg = red[256 + tid];
-      float c1v = 0.f, c0v = 0.f;
-      if (c < f.C) {
-        if (f.dbeta) f.dbeta[c] = f.accumulate ? f.dbeta[c] + (float)db : (float)db;
-        if (f.dgamma) f.dgamma[c] = f.accumulate ? f.dgamma[c] + (float)dg : (float)dg;
-        if (f.training) {
-          const double sc = scale[c], is = invstd[c], mu = mean[c];
-          const double c1 = -sc * is * dg / f.count;
-          c1v = (float)c1;
-          c0v = (float)(-sc * db / f.count - c1 * mu);
-        }
-      }
-      f.c1[c] = c1v;
-      f.c0[c] = c0v;
-    }
-  }
-}
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
 // (row, channel) {S1, S2, K, n} = sums of (y - K) and (y - K)^2 over the n
 // outputs the row's workgroup produced, K a pivot value taken from those
@@ -602,11 +352,6 @@ struct WGradArgs {
   // instruction and z taps on the column side (form 1)
   int ARS, w8mode, w8nbv, w8nj, w8nh;
   int w8off[128];                     // wgrad8 row (form 0) / row-quad (form 1) A image offsets
-  // BatchNorm-backward apply of the gradient operand on load (wgrad8 form 0,
-  // when the weight gradient is the apply's only consumer): G holds d(post-
-  // BN) dz and the operand is dz*g_scale + (g_c1*g_y + g_c0) per channel, the
-  // bits bn_bwd_apply would have stored; null: G is the operand itself.
-  const float *g_y, *g_scale, *g_c1, *g_c0;
   // ConvTranspose3d with kernel % stride == 0 as the weight gradient of its
   // phase-folded forward convolution (wgrad2, taps_rows): rows (j, ci) over
   // the J = K / S taps with A zero-padded by J - 1 (apx..), columns (phase q,
@@ -617,7 +362,6 @@ struct WGradArgs {
 };
 int plan_bwgrad(WGradArgs &a, int target_blocks);
 int launch_bwgrad(const WGradArgs &a, hipStream_t s);
-bool bwgrad_gap_ok(const WGradArgs &a);   // a GAP (operand-apply) instance exists
 int plan_wgrad(WGradArgs &a, int target_blocks);
 int plan_wgrad8(WGradArgs &a);
 int launch_wgrad8(const WGradArgs &a, hipStream_t s);
@@ -848,7 +592,7 @@ enum PrepKind { PREP_CONV_FWD = 0, PREP_CONV_DGRAD = 1, PREP_CONVT_FUSED = 2,
 struct PrepJob {
   int kind;
   short bf16;       // != 0: the prepared image is written as bf16 (bconv)
-  short tiled;      // set by launch_prep_all: the LDS-staged form (prep_all.hip)
+  short pad_;
   int64_t n;        // elements of the prepared buffer
   int64_t src;      // float offset of the PyTorch-layout weight in the parameter buffer
   int64_t dst;      // float offset of the prepared buffer in the destination workspace

@@ -123,87 +123,12 @@ __device__ __forceinline__ uint32_t prep_perm(uint32_t u, uint32_t nv, uint32_t 
   return (u % r) * cw + u / r;
 }
 
-// LDS-staged re-layout of a packed Conv3d image (forward or input-gradient,
-// groups == 1; prep_tiled): a workgroup owns one channel chunk x kPrepCT
-// image columns, reads the PyTorch-layout weights it needs once -- contiguous
-// runs, [o][e][t] order -- into LDS (the cat fold summed on the way, weff2's
-// order), then writes its 16-byte vectors in runs of kPrepCT consecutive
-// columns.  Same elements as prep_eval, bit for bit.  The gather form re-read
-// each weight line once per tap group from L2 / HBM (config 3: 114 MB fetched
-// per launch for 46 MB of parameters).
-constexpr int kPrepCT = 16;
-__device__ __forceinline__ int prep_tiles(const PrepJob &jb) {
-  return (jb.p[5] / jb.pk.CK) * ((jb.p[6] + kPrepCT - 1) / kPrepCT);
-}
-template <int V>
-__device__ void prep_tile(const PrepJob &jb, const float *w, float *dst, float *lw) {
-  const int *p = jb.p;
-  const int Cout = p[0], Cin_g = p[1], fold = p[3], T = p[4], CoutW = p[6], E = p[7];
-  const bool fwd = jb.kind == PREP_CONV_FWD;
-  const int CK = jb.pk.CK, S = jb.pk.S, CT = kPrepCT;
-  const int nct = (CoutW + CT - 1) / CT;
-  const int chunk = blockIdx.x / nct, col0 = (blockIdx.x % nct) * CT, k0 = chunk * CK;
-  // FWD: image row k = input channel e, column = output channel o: rows o (CT) x e (CK)
-  // DGRAD: image row k = output channel o, column = e: rows o (CK) x e (CT)
-  const int R = fwd ? CT : CK, C = fwd ? CK : CT;
-  const int tid = threadIdx.x;
-  for (int idx = tid; idx < R * C * T; idx += 256) {
-    const int t = idx % T, q = idx / T, c = q % C, r = q / C;
-    const int o = fwd ? col0 + r : k0 + r, e = fwd ? k0 + c : col0 + c;
-    float v = 0.f;
-    if (o < Cout && e < E)
-      for (int cp = e; cp < Cin_g; cp += fold) v += w[((size_t)o * Cin_g + cp) * T + t];
-    lw[idx] = v;
-  }
-  __syncthreads();
-  const int Cg = CK / V, TPS = 4 / Cg;
-  for (int u = tid; u < S * 4 * CT; u += 256) {
-    const int n = u % CT, sg = u / CT, g = sg & 3, s = sg >> 2;
-    const int col = col0 + n;
-    if (col >= CoutW) continue;
-    const int t = s * TPS + g / Cg, cl = (g % Cg) * V;
-    float v[V];
-#pragma unroll
-    for (int j = 0; j < V; ++j)
-      v[j] = t >= T ? 0.f
-                    : fwd ? lw[((size_t)n * CK + cl + j) * T + t] : lw[((size_t)(cl + j) * CT + n) * T + (T - 1 - t)];
-    const size_t vi = ((size_t)(chunk * S + s) * 4 + g) * CoutW + col;
-    if constexpr (V == 8)
-      reinterpret_cast<uint4 *>(dst)[vi] = make_uint4((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
-                                                      (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16),
-                                                      (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16),
-                                                      (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16));
-    else
-      reinterpret_cast<float4 *>(dst)[vi] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-// Whether a job takes the LDS-staged form (host side).
-static bool prep_tiled(const PrepJob &jb, size_t lds_cap_floats) {
-  if (jb.kind != PREP_CONV_FWD && jb.kind != PREP_CONV_DGRAD) return false;
-  if (jb.p[2] != 1 || jb.p[3] < 1 || jb.p[9]) return false;           // groups == 1, no parts
-  const bool bf = jb.bf16 && jb.pk.on == 3, f32 = !jb.bf16 && jb.pk.on == 1;
-  if (!bf && !f32) return false;
-  const int V = bf ? 8 : 4;
-  if (jb.pk.CK % V || jb.p[5] % jb.pk.CK || jb.pk.CoutW != jb.p[6] || (jb.dst & 3)) return false;
-  if ((4 / (jb.pk.CK / V)) * (jb.pk.CK / V) != 4) return false;          // whole taps per K-step
-  return (size_t)kPrepCT * jb.pk.CK * jb.p[4] <= lds_cap_floats;
-}
-
 __global__ void __launch_bounds__(256)
 prep_all_kernel(const float *params, float *dst_base, const PrepBatch b, int perm) {
-  extern __shared__ __attribute__((aligned(16))) float lw[];
   const PrepJob &jb = b.j[blockIdx.y];
   const float *w = params + jb.src;
   float *dst = dst_base + jb.dst;
   const uint32_t n = (uint32_t)jb.n;   // < 2^31 (launch_prep_all)
-  if (jb.tiled) {
-    if ((int)blockIdx.x >= prep_tiles(jb)) return;
-    if (jb.bf16)
-      prep_tile<8>(jb, w, dst, lw);
-    else
-      prep_tile<4>(jb, w, dst, lw);
-    return;
-  }
   // packed images: one decode per 16-byte vector (8 bf16 / 4 fp32 elements
   // whose middle index advances by one), one 16-byte store
   if (jb.pk.on && jb.kind != PREP_CONVT_PHASE && ((uintptr_t)dst & 15) == 0) {
@@ -253,36 +178,19 @@ prep_all_kernel(const float *params, float *dst_base, const PrepBatch b, int per
 int launch_prep_all(const float *params, float *dst_base, const PrepJob *jobs, int n,
                     hipStream_t s) {
   const int perm = 1;   // the tap-fastest vector order (prep_perm; round 3: config 3 -8..-18 us)
-  // HCU_PREP_TILED=1 (opt-in): the LDS-staged form where it applies; measured
-  // 22 -> 33 us per config-2 step and equal on config 3, so the gather stays
-  static const bool tiled = [] {
-    const char *e = getenv("HCU_PREP_TILED");
-    return e && e[0] == '1';
-  }();
   for (int j0 = 0; j0 < n; j0 += kPrepBatch) {
     PrepBatch b{};
     b.n = std::min(kPrepBatch, n - j0);
     int64_t most = 1;
-    int tiles = 1;
-    size_t lds = 0;
-    constexpr size_t kCap = 14336;   // 56 KB of staged weights per workgroup
     for (int k = 0; k < b.n; ++k) {
       b.j[k] = jobs[j0 + k];
       if (b.j[k].n >= (int64_t)1 << 31) return fail(4, "prep_all: weight image too large");
-      b.j[k].tiled = tiled && prep_tiled(b.j[k], kCap) ? 1 : 0;
-      if (b.j[k].tiled) {
-        const PrepJob &jb = b.j[k];
-        tiles = std::max(tiles, (jb.p[5] / jb.pk.CK) * ((jb.p[6] + kPrepCT - 1) / kPrepCT));
-        lds = std::max(lds, (size_t)kPrepCT * jb.pk.CK * jb.p[4] * sizeof(float));
-      } else {
-        most = std::max(most, b.j[k].n);
-      }
+      most = std::max(most, b.j[k].n);
     }
     // enough workgroups that the largest gathered job is ~8 elements per thread
-    const int gx = std::max(tiles, (int)std::max<int64_t>(1, std::min<int64_t>((most + 2047) / 2048, 1024)));
+    const int gx = (int)std::max<int64_t>(1, std::min<int64_t>((most + 2047) / 2048, 1024));
     HCU_TIMED(s, "prep_all_kernel", 0.0, 0.0,
-              HCU_LAUNCH(prep_all_kernel, dim3(gx, b.n), dim3(256), (uint32_t)lds, s, params,
-                                 dst_base, b, perm));
+              HCU_LAUNCH(prep_all_kernel, dim3(gx, b.n), dim3(256), 0, s, params, dst_base, b, perm));
     HCU_CHECK_LAUNCH();
   }
   return 0;

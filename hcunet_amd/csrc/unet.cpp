@@ -45,7 +45,6 @@ using namespace hcu;
 namespace {
 
 constexpr int kTargetBlocks = 1024;
-bool tails_enabled();   // (BnbFin last-workgroup finalizes, below)
 
 // Activation tensor dims.  es = element bytes: 4 (fp32 path, channel stride a
 // multiple of 4 = 16 bytes) or 2 (bf16 path, channel stride a multiple of 8).
@@ -453,16 +452,9 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
   }
   u.wg_phase = false;
   // The weight gradient of the phase-folded forward (stride phases as extra
-  // output columns): on wgrad3 by default, its bias from chansum (the mode-3
-  // finalize's serial bias sum over the phases is slow); HCU_CONVT_PHASE_WG=1:
-  // on wgrad2 with the bias row (measured +13 us per config-2 step against
-  // the per-tap wgrad_kernel + chansum: its wider slabs double the finalize
-  // reads), =0: off.  (The wgrad2 form only for u2.up / u3.up, where wgrad3
-  // does not apply -- fewer than 32 output channels: u2.up 30 -> 16 us and
-  // u3.up 30 -> 17 us with their chansums, and still 2.105-2.128 vs
-  // 2.059-2.072 ms per config-2 step, interleaved, 3 runs: their finalizes.)
-  static const int phase_mode = getenv("HCU_CONVT_PHASE_WG") ? atoi(getenv("HCU_CONVT_PHASE_WG")) : 2;
-  if (!bf && u.fused && o % 4 == 0 && phase_mode) {
+  // output columns) on wgrad3, its bias from chansum; the other layers run the
+  // per-tap wgrad_kernel + chansum.
+  if (!bf && u.fused && o % 4 == 0) {
     // dW'[(j, ci)][(q, co)] = sum_o A[o + j - (J-1)][ci] * dU[o*S + q][co] over the
     // phase grid o (the forward's fused GEMM, hcat/unet.py:294-298)
     const int J[3] = {u.K[0] / u.S[0], u.K[1] / u.S[1], u.K[2] / u.S[2]};
@@ -478,9 +470,9 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     w.gsx = u.S[0]; w.gsy = u.S[1]; w.gsz = u.S[2];
     w.gdx = w.gdy = w.gdz = 1;
     w.taps_rows = 1;
-    w.bias_row = phase_mode == 1 ? 1 : 0;
+    w.bias_row = 0;
     w.nph = nph; w.phx = u.S[0]; w.phy = u.S[1]; w.phz = u.S[2]; w.GCout = o;
-    if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == (phase_mode == 1 ? 1 : 3)) {
+    if (plan_wgrad(w, kTargetBlocks) == 0 && w.v2 == 3) {
       u.wgp = w;
       u.wg_phase = true;
       max_part = std::max(max_part, wgrad_partial_floats(w));
@@ -494,7 +486,6 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
 }  // namespace
 
 #define HCU_NBUF 32   // gradient slots (at most; Ctx::alloc)
-constexpr int kCtrPerSite = 64;   // BnbFin ticket counters per producing launch (column groups)
 #define HCU_NBUF_RING 6   // ring size when one slot per allocation does not fit
 #define HCU_FORK_RING 16   // marker events of forks that cannot use the chain record
 
@@ -530,8 +521,6 @@ struct hcu_unet_plan {
   int nbuf = HCU_NBUF_RING;
   bool no_reuse = false;
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
-  size_t fin_off = 0;   // finalize ticket counters (HCU_BNFIN forward; BnbFin tails of the backward)
-  int n_ctr_sites = 0;  // BnbFin counter blocks (kCtrPerSite words each)
   double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
   // Layer-chain plans (hcu_chain_*): a sequence of ops instead of the U-Net.
   struct ChainOp {
@@ -857,11 +846,6 @@ int build_plan(hcu_unet_plan &p) {
   p.wpart_off = scratch.take_floats(p.wpart_floats);
   p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
-  // one counter block per BatchNorm layer's backward finalize (+ slack)
-  // (counters only for the opt-in last-workgroup finalizes: no memset per
-  // backward otherwise)
-  p.n_ctr_sites = fwd_only || !tails_enabled() ? 0 : p.n_bn + 4;
-  p.fin_off = scratch.take_floats(std::max<size_t>(16, (size_t)p.n_ctr_sites * kCtrPerSite));
   p.scratch_bytes = scratch.off;
   if (getenv("HCU_PLAN_LOG")) {   // weight-gradient kernels and their partial slabs (measurement)
     auto wlog = [](const std::string &n, const WGradArgs &w) {
@@ -927,25 +911,6 @@ struct Ctx {
     return 0;
   }
   float *wprep() const { return fptr(sc, p.wprep_off); }
-  // Ticket counters of the BatchNorm-backward finalize tails (BnbFin): one
-  // block of kCtrPerSite words per producing launch, all zeroed by one memset
-  // at the start of the backward (zero_counters) and left at zero by each
-  // launch's last workgroup.
-  int ctr_next = 0;
-  unsigned *counters(int n) {
-    if (n > kCtrPerSite || ctr_next >= p.n_ctr_sites) return nullptr;   // no tail: separate finalize
-    unsigned *r = reinterpret_cast<unsigned *>(sc + p.fin_off) + (size_t)ctr_next * kCtrPerSite;
-    ++ctr_next;
-    return r;
-  }
-  int zero_counters() {
-    if (p.n_ctr_sites) HCU_HIP(hipMemsetAsync(sc + p.fin_off, 0, (size_t)p.n_ctr_sites * kCtrPerSite * 4, s));
-    return 0;
-  }
-  // Layers whose dY = dz*scale + c1*y + c0 is not materialised: their
-  // consumers (weight and input gradient) apply it on load (ap_ok).
-  unsigned long long ap_mask = 0;
-  bool ap(const ConvLayer &L) const { return (ap_mask >> L.bn.index) & 1ull; }
   float *buf(int i) const { return fptr(sc, p.buf_off[i]); }
   float *kpart() const { return fptr(sc, p.kpart_off); }
   hipStream_t wstream() const { return split ? ws : s; }
@@ -1012,26 +977,6 @@ void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
 }
 
-// HCU_BNB_TAIL=1 (opt-in): the BatchNorm-backward finalize in the producing
-// dgrad's last workgroup (BnbFin) instead of the bn_bwd_finalize launch;
-// measured +10 us per config-2 step (the last workgroup's serial reduction
-// costs more than the launch it removes)
-bool tails_enabled() {
-  static const bool on = getenv("HCU_BNB_TAIL") && getenv("HCU_BNB_TAIL")[0] == '1';
-  return on;
-}
-
-// rows x channels a finalize tail may read
-long tail_max_values() {
-  static const long v = 4096;
-  return v;
-}
-
-bool bnfin_enabled() {
-  static const bool on = getenv("HCU_BNFIN") && getenv("HCU_BNFIN")[0] == '1';
-  return on;
-}
-
 int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float *isc,
                  const float *ish, int training) {
   HCU_HIP(hipGetLastError());
@@ -1046,28 +991,6 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   a.stats = training ? c.part() : nullptr;
   a.partial = c.kpart();
   const BNCoef coef = coef_at(c.sv, L.bn);
-  // training bconv, opt-in (HCU_BNFIN=1): the BatchNorm finalize in the conv's
-  // last workgroup.  Measured slower (+35..60 us per layer on MI355X: every
-  // workgroup's agent-scope release fence writes back its XCD's L2), so the
-  // separate finalize launch stays the default.
-  if (training && a.use_bconv && bnfin_enabled() && a.lds_bytes - (int)sizeof(GConvArgs) >= 6144) {
-    BnFin &f = a.fin;
-    f.gamma = c.P + L.bn.gamma;
-    f.beta = c.P + L.bn.beta;
-    f.rm = c.t.bn_running_mean[L.bn.index];
-    f.rv = c.t.bn_running_var[L.bn.index];
-    f.nbt = c.t.bn_num_batches_tracked[L.bn.index];
-    f.coef = coef;
-    f.count = L.bn.count;
-    f.eps = c.p.spec.bn_eps;
-    f.momentum = c.p.spec.bn_momentum;
-    f.C = L.bn.C;
-    f.Cs = L.bn.Cs;
-    f.R = gconv_rows(L.fwd);
-    f.W = L.fwd.CoutW;
-    f.counter = reinterpret_cast<unsigned *>(c.fptr(c.sc, c.p.fin_off));
-    return launch_conv_any(a, c.s);
-  }
   if (int e = launch_conv_any(a, c.s)) return e;
   return launch_bn_fwd_finalize(c.part(), gconv_rows(L.fwd), L.fwd.CoutW, L.bn.C, L.bn.Cs,
                                 L.bn.count, c.P + L.bn.gamma, c.P + L.bn.beta,
@@ -1078,10 +1001,8 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
 
 // Sets up the dgrad epilogue that also performs the BatchNorm+ReLU backward
 // reduction of layer `bnl` (whose output the gradient is for); false when the
-// planned kernel cannot.  When the kernel can also finalize in its last
-// workgroup (BnbFin: bconv, its K-split reduce) and a counter block is free,
-// the separate bn_bwd_finalize launch is dropped (finish_bnbwd).
-bool fuse_bnbwd(Ctx &c, GConvArgs &a, const ConvLayer *bnl, int training, int accumulate) {
+// planned kernel cannot.
+bool fuse_bnbwd(Ctx &c, GConvArgs &a, const ConvLayer *bnl) {
   static const bool off = getenv("HCU_NO_BNFUSE") != nullptr;   // A/B debugging
   if (off || !bnl || !conv_bnbwd_fusable(a)) return false;
   const BNCoef coef = coef_at(c.sv, bnl->bn);
@@ -1091,97 +1012,37 @@ bool fuse_bnbwd(Ctx &c, GConvArgs &a, const ConvLayer *bnl, int training, int ac
   a.bn_mean = coef.mean;
   a.bn_invstd = coef.invstd;
   a.stats = c.part();
-  a.bfin = BnbFin{};
-  // The last workgroup reads every row of its column group: worth it (vs the
-  // separate finalize launch) only when that is a couple of loads per thread.
-  const int groups = a.ksplit > 1 ? 1 : a.CoutW / (a.NSUB * 16);
-  const long tail_vals = (long)gconv_rows(a) * (a.ksplit > 1 ? a.OCs : a.NSUB * 16);
-  if (a.use_bconv && tails_enabled() && tail_vals <= tail_max_values()) {
-    if (unsigned *ctr = c.counters(groups)) {
-      BnbFin &f = a.bfin;
-      f.dgamma = c.G + bnl->bn.gamma;
-      f.dbeta = c.G + bnl->bn.beta;
-      f.c1 = coef.c1;
-      f.c0 = coef.c0;
-      f.count = bnl->bn.count;
-      f.C = bnl->bn.C;
-      f.training = training;
-      f.accumulate = accumulate;
-      f.counter = ctr;
-    }
-  }
   return true;
 }
 
-// Finalize (unless the producing kernel did it in its last workgroup) and
-// apply (unless bnl's consumers apply it on load, Ctx::ap) of a BatchNorm
-// backward whose reduction rows are in c.part().
-int finish_bn(const Ctx &c, const ConvLayer &bnl, int R, int W, bool tail_done, float *dz, int training,
-              int accumulate) {
+// Finalize and apply of a BatchNorm backward whose reduction rows are in
+// c.part(): dz -> dY of bnl in place.
+int finish_bn(const Ctx &c, const ConvLayer &bnl, int R, int W, float *dz, int training, int accumulate) {
   const BNCoef coef = coef_at(c.sv, bnl.bn);
-  if (!tail_done)
-    if (int e = launch_bn_bwd_finalize(c.part(), R, bnl.bn.C, bnl.bn.Cs, W, bnl.bn.count, coef,
-                                       c.G + bnl.bn.gamma, c.G + bnl.bn.beta, training, accumulate, c.s))
-      return e;
-  if (c.ap(bnl)) return 0;
+  if (int e = launch_bn_bwd_finalize(c.part(), R, bnl.bn.C, bnl.bn.Cs, W, bnl.bn.count, coef,
+                                     c.G + bnl.bn.gamma, c.G + bnl.bn.beta, training, accumulate, c.s))
+    return e;
   return launch_bn_bwd_apply(dz, c.fptr(c.sv, bnl.y_off), coef, bnl.out.vox(), bnl.out.Cs, c.s, c.bf());
 }
 
 int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *dz, int training,
                  int accumulate) {
-  return finish_bn(c, bnl, gconv_rows(a), a.CoutW, a.bfin.counter != nullptr, dz, training, accumulate);
-}
-
-// Whether layer L's consumers -- its weight gradient and, when planned, its
-// input gradient -- can apply the BatchNorm backward on load (dz*scale +
-// c1*y + c0 while staging the operand), so dY(L) is never materialised: the
-// input gradient on bconv (AP instances), the weight gradient on wgrad2,
-// wgrad8 form 0 or the pipelined bwgrad.  Opt-in (HCU_AP=1): measured on
-// MI355X, every qualifying layer +27 us per config-2 step (-20 us on config 3
-// in one run) -- a consumer staging dz and y runs 15-40 % longer, which costs
-// what the apply pass and its launch save -- and the first layer's weight
-// gradient alone (the round-3 default) +7 us per config-2 step.
-bool ap_ok(const Ctx &c, const ConvLayer &L, bool with_dgrad) {
-  static const int mode = getenv("HCU_AP") ? atoi(getenv("HCU_AP")) : 0;
-  // the largest dY (bytes) applied on load
-  static const double max_b = 8e6;
-  if (mode == 0 || c.p.is_chain || L.bn.index >= 64) return false;
-  const WGradArgs &w = L.wg;
-  const bool small = (double)L.out.vox() * L.out.Cs * L.out.es <= max_b;
-  if (with_dgrad && (!small || !L.dgrad.use_bconv)) return false;
-  // (the bf16 first layer's bwgrad with the operand apply ran 253 us against
-  // 115 + 116 for bwgrad + the apply pass: only small bf16 layers)
-  if (w.use_bw) return small && bwgrad_gap_ok(w);
-  if (w.v2 == 2) return w.w8mode == 0 && w.GCs <= 16 && (small || !with_dgrad);
-  return w.v2 == 1 && small;
-}
-// Decides (once, before dz(L) is produced) whether L's dY stays unmaterialised.
-void decide_ap(Ctx &c, const ConvLayer &L, bool with_dgrad) {
-  if (ap_ok(c, L, with_dgrad)) c.ap_mask |= 1ull << L.bn.index;
+  return finish_bn(c, bnl, gconv_rows(a), a.CoutW, dz, training, accumulate);
 }
 
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
-// dy holds dY of L, or dz of L when Ctx::ap(L) (applied on load by both
-// consumers).  With `bnl`, the input gradient leaves as dz of layer bnl (its
-// BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
+// dy holds dY of L.  With `bnl`, the input gradient leaves as dz of layer bnl
+// (its BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
                   const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
-  const bool ap = c.ap(L);
-  const BNCoef lc = coef_at(c.sv, L.bn);
   WGradArgs w = L.wg;
   w.A = A;
   w.a_scale = asc;
   w.a_shift = ash;
   w.G = dy;
-  if (ap) {   // dy holds dz of L's BatchNorm: applied on load
-    w.g_y = c.fptr(c.sv, L.y_off);
-    w.g_scale = lc.scale;
-    w.g_c1 = lc.c1;
-    w.g_c0 = lc.c0;
-  }
   if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
   if (int e = launch_wgrad(w, c.wstream())) return e;
   WGradFinalize f{};
@@ -1207,16 +1068,10 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   tag(L.name, "dgrad");
   GConvArgs a = L.dgrad;
   a.in = dy;
-  if (ap) {
-    a.in_y = c.fptr(c.sv, L.y_off);
-    a.in_scale = lc.scale;
-    a.in_shift = lc.c1;
-    a.in_c0 = lc.c0;
-  }
   a.w = c.fptr(c.sv, L.wd_off);
   a.out = dA;
   a.partial = c.kpart();
-  const bool fused = fuse_bnbwd(c, a, bnl, training, accumulate);
+  const bool fused = fuse_bnbwd(c, a, bnl);
   if (int e = launch_conv_any(a, c.s)) return e;
   if (!fused) return 0;
   tag(bnl->name, "bnbwd");
@@ -1245,7 +1100,7 @@ int bn_backward(const Ctx &c, const ConvLayer &L, float *dbuf, const float *pool
                                            c.bf()))
       return e;
   }
-  return finish_bn(c, L, R, L.bn.Cs, false, dbuf, training, accumulate);
+  return finish_bn(c, L, R, L.bn.Cs, dbuf, training, accumulate);
 }
 
 }  // namespace
@@ -1459,9 +1314,6 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   c.ws = split ? p.side : c.s;
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
-  // the fused-finalize ticket counters (HCU_BNFIN) start from 0: a memset only then
-  // (a packet on the chain costs ~3 us of GPU time)
-  if (training && bnfin_enabled()) HCU_HIP(hipMemsetAsync(c.fptr(c.sc, p.fin_off), 0, 64, c.s));
   tag(std::string("in"), "fwd");
   if (!input_done)
     if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
@@ -1632,14 +1484,12 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(),
                                 c.s))
       return e;
-  if (int e = c.zero_counters()) return e;
   int cur = 0;  // slot holding the current d(pre-BN y) (or dz, Ctx::ap)
   if (int e = c.alloc(cur)) return e;
 
   // out_conv + last BatchNorm
   const ConvLayer &last = p.uc2[p.L - 2];
   tag(std::string("out"), "bwd");
-  decide_ap(c, last, true);
   {
     const BNCoef coef = coef_at(c.sv, last.bn);
     const int64_t nvox = last.out.vox();
@@ -1653,7 +1503,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = launch_outconv_wfinalize(part_oc, R, p.Co, last.out.C, last.out.Cs, c.G + p.oc_w,
                                          c.G + p.oc_b, accumulate, c.s))
       return e;
-    if (int e = finish_bn(c, last, R, last.bn.Cs, false, c.buf(cur), training, accumulate)) return e;
+    if (int e = finish_bn(c, last, R, last.bn.Cs, c.buf(cur), training, accumulate)) return e;
   }
   // decoder, last to first
   for (int j = p.L - 2; j >= 0; --j) {
@@ -1666,7 +1516,6 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.alloc(sb)) return e;
     float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
-    decide_ap(c, c1, true);
     if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
                               accumulate, &c1, training, &done1))
       return e;
@@ -1776,8 +1625,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       a.w = c.fptr(c.sv, u.wd_off);
       a.out = dP;
       a.partial = c.kpart();
-      decide_ap(c, prev, true);
-      const bool fused = fuse_bnbwd(c, a, &prev, training, accumulate);
+      const bool fused = fuse_bnbwd(c, a, &prev);
       if (int e = launch_conv_any(a, c.s)) return e;
       if (fused) {
         tag(prev.name, "bnbwd");
@@ -1809,9 +1657,6 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.alloc(sb)) return e;
     float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
-    // (the first layer without an input gradient: its weight gradient is the
-    // only consumer of dz(y1))
-    decide_ap(c, c1, i > 0 || dx);
     if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
                               accumulate, &c1, training, &done1))
       return e;
@@ -1829,7 +1674,6 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       // dIn = d(pooled): produce d(pre-BN y2_{i-1}) into a fresh slot
       int sp = 0;
       if (int e = c.alloc(sp)) return e;
-      decide_ap(c, p.dc2[i - 1], true);
       if (int e = bn_backward(c, p.dc2[i - 1], c.buf(sp), dIn, s.pool_k, training, accumulate))
         return e;
       cur = sp;
@@ -2388,7 +2232,6 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
   p.wpart_off = scratch.take_floats(p.wpart_floats);
   p.wprep_off = scratch.take_floats(p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
-  p.fin_off = scratch.take_floats(16);
   p.ufull_off = scratch.take_floats(p.max_ufull);
   for (size_t &o : p.sub_off) o = scratch.take_floats(p.max_sub);
   p.scratch_bytes = scratch.off;
@@ -2659,7 +2502,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       g.out = dP;
       g.partial = c.kpart();
       const ConvLayer *bnl = (pr && pr->kind == HCU_CHAIN_CONV && pr->bn_relu) ? &pr->conv : nullptr;
-      const bool fused = fuse_bnbwd(c, g, bnl, training, accumulate);
+      const bool fused = fuse_bnbwd(c, g, bnl);
       if (int e = launch_conv_any(g, s)) return e;
       if (fused)
         if (int e = finish_bnbwd(c, g, *bnl, dP, training, accumulate)) return e;

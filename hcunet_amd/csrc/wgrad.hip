@@ -402,16 +402,6 @@ __global__ void __launch_bounds__(256) wgrad2_kernel(const WGradArgs a) {
             const size_t go = ((((size_t)b * a.GX + gx * a.gsx + gq[0]) * a.GY + gy * a.gsy + gq[1]) * a.GZ +
                                gz * a.gsz + gq[2]) * a.GCs + c;
             val[u] = *reinterpret_cast<const float4 *>(a.G + go);
-            if (a.g_y) {   // G holds dz: the BatchNorm backward applied on load (bn_bwd_apply's bits)
-              const float4 yv = *reinterpret_cast<const float4 *>(a.g_y + go);
-              const float4 sc = *reinterpret_cast<const float4 *>(a.g_scale + c);
-              const float4 c1 = *reinterpret_cast<const float4 *>(a.g_c1 + c);
-              const float4 c0 = *reinterpret_cast<const float4 *>(a.g_c0 + c);
-              val[u].x = fmaf(val[u].x, sc.x, fmaf(c1.x, yv.x, c0.x));
-              val[u].y = fmaf(val[u].y, sc.y, fmaf(c1.y, yv.y, c0.y));
-              val[u].z = fmaf(val[u].z, sc.z, fmaf(c1.z, yv.z, c0.z));
-              val[u].w = fmaf(val[u].w, sc.w, fmaf(c1.w, yv.w, c0.w));
-            }
           }
         }
       }

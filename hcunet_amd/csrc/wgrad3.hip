@@ -299,7 +299,7 @@ int plan_wgrad3(WGradArgs &a) {
   if (ph && a.bias_row) return 1;   // (its bias comes from chansum)
   // (16-channel inputs stay on wgrad2: d2.c1 of config 2 ran 65 us here
   // against 52 us there; every wider layer measured faster here)
-  if (a.ACs % 32 || a.g_y) return 1;
+  if (a.ACs % 32) return 1;
   // 32-bit buffer offsets within one sample
   if ((double)a.AX * a.AY * a.AZ * a.ACs >= (double)(1 << 29) || (double)a.GX * a.GY * a.GZ * a.GCs >= (double)(1 << 29))
     return 1;

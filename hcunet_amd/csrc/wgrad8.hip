@@ -35,13 +35,11 @@ namespace hcu {
 // MODE 0: NR = row tiles of 16 (rows (kx,ky,ci) + bias).  MODE 1: NR = row
 // quads per wave; the plan's a.MS quads ((kx,ky,ci quad) + the bias quad last)
 // are split over a.w8nh wave groups, each taking every (4/w8nh)-th K-step.
-// GAP: the gradient operand is BatchNorm-backward applied on load (a.g_y).
-template <int MODE, int NR, bool GAP>
+template <int MODE, int NR>
 __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ __attribute__((aligned(16))) char sa_raw[sizeof(WGradArgs)];
   __shared__ __attribute__((aligned(16))) float actl[2][32];  // BN scale / shift of this chunk
-  __shared__ __attribute__((aligned(16))) float gapl[3][16];  // GAP: scale, c1, c0 per G channel
   WGradArgs &sa = *reinterpret_cast<WGradArgs *>(sa_raw);
 #define KA(f) kuni(sa.f)
   const int tid = threadIdx.x, lane = tid & 63;
@@ -66,11 +64,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
   if (tid < CKA) {
     actl[0][tid] = act ? a.a_scale[ci0 + tid] : 1.f;
     actl[1][tid] = act ? a.a_shift[ci0 + tid] : 0.f;
-  }
-  if (GAP && tid < GCs) {
-    gapl[0][tid] = a.g_scale[tid];
-    gapl[1][tid] = a.g_c1[tid];
-    gapl[2][tid] = a.g_c0[tid];
   }
 
   lds_barrier();
@@ -144,10 +137,7 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
     }
   }
   floatx4 ra[2][4], rg[2][4];
-  constexpr int NGY = GAP ? 2 : 1;
-  floatx4 ry[NGY][4];                                // GAP: the BatchNorm input y at the G positions
   int ma = 0;                                        // valid A voxels: bit u*4 + j
-  int mg = 0;                                        // GAP: valid G voxels: bit u*4 + j
 
   // Branch-free buffer loads straight into the prefetch registers (a load under
   // a branch is copied at the join, which waits for it): invalid positions read
@@ -186,9 +176,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
     const size_t sampG = (size_t)GX * GY * GZ * GCs;
     const __amdgpu_buffer_rsrc_t rsG =
         __builtin_amdgcn_make_buffer_rsrc((void *)(KA(G) + b * sampG), 0, (int)(sampG * 4), 0x00020000);
-    __amdgpu_buffer_rsrc_t rsY = rsG;
-    if (GAP) rsY = __builtin_amdgcn_make_buffer_rsrc((void *)(KA(g_y) + b * sampG), 0, (int)(sampG * 4), 0x00020000);
-    mg = 0;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int ig = tid + u * 256;
@@ -204,11 +191,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
         const bool ok = okc && z >= 0 && z < PZ;
         rg[u][j] = __builtin_bit_cast(floatx4,
                                       __builtin_amdgcn_raw_buffer_load_b128(rsG, ok ? base + j * GCs * 4 : OOB, 0, 0));
-        if (GAP) {
-          ry[u & (NGY - 1)][j] = __builtin_bit_cast(
-              floatx4, __builtin_amdgcn_raw_buffer_load_b128(rsY, ok ? base + j * GCs * 4 : OOB, 0, 0));
-          mg |= (ok ? 1 : 0) << (u * 4 + j);
-        }
       }
     }
   };
@@ -241,19 +223,6 @@ __global__ void __launch_bounds__(256, 2) wgrad8_kernel(const WGradArgs a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (gdst[u] < 0) continue;
-      if (GAP) {   // dy = dz*scale + (c1*y + c0), bn_bwd_apply's expression; 0 outside
-        const int cq = (tid + u * 256) % CG4;
-        const floatx4 gs = *reinterpret_cast<const floatx4 *>(&gapl[0][cq * 4]);
-        const floatx4 g1 = *reinterpret_cast<const floatx4 *>(&gapl[1][cq * 4]);
-        const floatx4 g0 = *reinterpret_cast<const floatx4 *>(&gapl[2][cq * 4]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool ok = (mg >> (u * 4 + j)) & 1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            rg[u][j][e] = ok ? fmaf(rg[u][j][e], gs[e], fmaf(g1[e], ry[u & (NGY - 1)][j][e], g0[e])) : 0.f;
-        }
-      }
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         *reinterpret_cast<floatx4 *>(glds + gdst[u] + c * GPL) =
@@ -573,15 +542,10 @@ int launch_wgrad8(const WGradArgs &a, hipStream_t s) {
   const double by = 4.0 * ((double)a.B * a.AX * a.AY * a.AZ * a.ACs +
                            (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
   bool ok = false;
-  if (a.g_y && (a.w8mode != 0 || a.GCs > 16)) return fail(4, "wgrad8: operand apply needs form 0");
 #define W8(MODE_, NR_)                                                                                    \
   if (!ok && a.w8mode == MODE_ && a.MS == NR_) {                                                          \
-    if (a.g_y)                                                                                            \
-      HCU_TIMED(s, "wgrad8_kernel<" #MODE_ "," #NR_ ",gap>", fl, by,                                      \
-                HCU_LAUNCH((wgrad8_kernel<MODE_, NR_, true>), grid, dim3(256), a.lds_bytes, s, a)); \
-    else                                                                                                  \
-      HCU_TIMED(s, "wgrad8_kernel<" #MODE_ "," #NR_ ">", fl, by,                                          \
-                HCU_LAUNCH((wgrad8_kernel<MODE_, NR_, false>), grid, dim3(256), a.lds_bytes, s, a)); \
+    HCU_TIMED(s, "wgrad8_kernel<" #MODE_ "," #NR_ ">", fl, by,                                            \
+              HCU_LAUNCH((wgrad8_kernel<MODE_, NR_>), grid, dim3(256), a.lds_bytes, s, a));           \
     ok = true;                                                                                            \
   }
   W8(0, 1) W8(0, 2) W8(0, 3) W8(0, 4) W8(0, 5) W8(0, 6) W8(0, 7) W8(0, 8)
@@ -589,7 +553,7 @@ int launch_wgrad8(const WGradArgs &a, hipStream_t s) {
 #define W8Q(NRW_)                                                                             \
   if (!ok && a.w8mode == 1 && cdiv(a.MS, a.w8nh) == NRW_) {                                   \
     HCU_TIMED(s, "wgrad8_kernel<1," #NRW_ ">", fl, by,                                        \
-              HCU_LAUNCH((wgrad8_kernel<1, NRW_, false>), grid, dim3(256), a.lds_bytes, s, a)); \
+              HCU_LAUNCH((wgrad8_kernel<1, NRW_>), grid, dim3(256), a.lds_bytes, s, a));        \
     ok = true;                                                                                \
   }
   W8Q(2) W8Q(3) W8Q(4) W8Q(5) W8Q(6) W8Q(7) W8Q(8) W8Q(9) W8Q(10)

@@ -3,7 +3,7 @@
 # runs bench.py (no CPU baseline, no per-kernel timing pass) REPS times,
 # alternating arms, and the ms/step of every run is printed.
 #   bash tools/gpu_abx.sh TAG CONFIG REPS 'ENV_A' 'ENV_B' ['ENV_C' ...]
-# e.g. bash tools/gpu_abx.sh ab1 2 3 'HCU_AP=0' 'HCU_AP=1'
+# e.g. bash tools/gpu_abx.sh ab1 2 3 'HCU_WGRAD3=0' 'HCU_WGRAD3=1'
 set -o pipefail
 TAG=$1; CFG=$2; REPS=$3; shift 3
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
