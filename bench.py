@@ -460,6 +460,9 @@ def main():
                     help='tiled inference driver throughput (SURVEY 8f-1) instead of training')
     ap.add_argument('--runet', action='store_true',
                     help='BASELINE config 5: r_unet.py RDCNet training on 512x512x24 tiles (bf16)')
+    ap.add_argument('--input-dtype', default='fp32', choices=['fp32', 'fp16', 'bf16'],
+                    help='dtype of the [B,4,X,Y,Z] input volume handed to forward (16-bit confocal '
+                         'volumes: bf16 configs only, read directly by the first convolution)')
     args = ap.parse_args()
     if args.infer:
         return infer_main(args)
@@ -483,6 +486,11 @@ def main():
     x, mask, pwl = synth_inputs(B, 1000 + rank, device)
 
     bf16 = cfg['dtype'] == 'bf16'
+    if args.input_dtype != 'fp32':
+        if not bf16:
+            raise SystemExit('--input-dtype %s: 16-bit input volumes need a bf16 config (the fp32 '
+                             'reference path raises on them)' % args.input_dtype)
+        x = x.to(torch.float16 if args.input_dtype == 'fp16' else torch.bfloat16)
 
     def step():
         opt.zero_grad()
@@ -592,6 +600,7 @@ def main():
                 "config": {"workload": "%s train step (fwd + pixel BCE + bwd + Adam), B=%d per "
                                        "GPU, %dx%dx%dx4 volumes" % ((cfg['desc'], B) + TILE),
                            "global_batch": B * world, "per_gpu_batch": B,
+                           "input_dtype": args.input_dtype,
                            "parallelism": "dp%d" % world, "final_loss": final_loss,
                            "host_enqueue_ms_per_step": t_enq / args.steps * 1e3},
                 "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,

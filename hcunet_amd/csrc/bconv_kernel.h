@@ -136,10 +136,21 @@ __device__ __forceinline__ floatx4 bload4(float *, __amdgpu_buffer_rsrc_t r, int
   return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 0));
 }
 
-// MODE 1 (BNB): the fused BatchNorm+ReLU backward epilogue.
+// MODE 1 (BNB): the fused BatchNorm+ReLU backward epilogue.  MODE 2 (NCX,
+// CV = 1, forward of the network's first layer): the input is the caller's
+// NCXYZ volume (GConvArgs::in_fmt fp32 / fp16 / bf16, <= 4 channels): each
+// halo element gathers its channels from the channel planes (consecutive
+// lanes: consecutive z, then y -- one contiguous run of a plane per wave),
+// converts them to E when the halo image is written (the rounding the
+// channels-last layout pass applies), stores the channels-last copy of the
+// voxels its tile owns (a.xcl), and the weights are read in their PyTorch
+// layout [Cout][in_c][T] (no packed image: the first layer runs ahead of the
+// weight re-layout).
 template <class E, int CV, int NSUB, int MPW, int NPF, int MODE>
 __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   constexpr bool BNB = (MODE & 1) != 0;
+  constexpr bool NCX = MODE == 2;
+  static_assert(!NCX || (CV == 1 && NPF > 0), "NCXYZ staging: one 16-byte group, prefetched");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // launch constants for the tile loop, read through kuni (common.h): they are
   // live only in the phase that uses them, not for the whole kernel
@@ -234,6 +245,23 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   };
   auto stage_w = [&](int chunk) {
     const int n16 = S * 4 * NT;
+    if constexpr (NCX) {   // PyTorch-layout weights: 16 bytes = channels 0..VEC-1 of tap sg, column n
+      const int INC = KA(in_c), Cout = KA(Cout);
+      const float *wr = KA(w);
+      for (int idx = tid; idx < n16; idx += 256) {
+        const int n = idx % NT, t = idx / NT, co = blockIdx.y * NT + n;
+        float v[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) v[j] = (t < T && co < Cout && j < INC) ? wr[((size_t)co * INC + j) * T + t] : 0.f;
+        if constexpr (ES == 2) {
+          reinterpret_cast<uint4 *>(wlds)[idx] = pack8(v);
+        } else {
+          reinterpret_cast<uint4 *>(wlds)[idx] = make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                                            __float_as_uint(v[2]), __float_as_uint(v[3]));
+        }
+      }
+      return;
+    }
     const uint4 *src = reinterpret_cast<const uint4 *>(KA(w));
     const int CoutW = KA(CoutW);
     for (int idx = tid; idx < n16; idx += 256) {
@@ -300,9 +328,40 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   uint32_t okbits = 0;
   // halo of (tile, chunk) -> pf (branch-free: the validity of each element is
   // a mask, invalid elements read offset 0x7ffffff0, outside the buffer -> 0)
+  // NCXYZ input (NCX): element u's channels from the planes; the raw loaded
+  // values (fp32 bits or a 16-bit value) in pf[u].x..w, converted when written
+  auto fetch_ncx = [&](int b, int x0, int y0, int z0, int IX, int IY, int IZ, int INC, int fmt) {
+    const int ESI = fmt == 1 ? 4 : 2;
+    const int plane = IX * IY * IZ;
+    const char *bp = reinterpret_cast<const char *>(KA(in)) + (size_t)b * INC * plane * ESI;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, INC * plane * ESI, 0x00020000);
+    okbits = 0;
+#pragma unroll
+    for (int u = 0; u < NPFR; ++u) {
+      const int hp = hpk[u];
+      const int gx = x0 + (hp >> 20), gy = y0 + ((hp >> 10) & 1023), gz = z0 + (hp & 1023);
+      const bool ok = (hp >= 0) & ((unsigned)gx < (unsigned)IX) & ((unsigned)gy < (unsigned)IY) &
+                      ((unsigned)gz < (unsigned)IZ);
+      const int vo = (gx * IY + gy) * IZ + gz;
+      uint32_t r[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int off = (ok && c < INC) ? (c * plane + vo) * ESI : 0x7ffffff0;
+        r[c] = fmt == 1 ? __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0)
+                        : (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0);
+      }
+      pf[u] = make_uint4(r[0], r[1], r[2], r[3]);
+      okbits |= (uint32_t)ok << u;
+    }
+  };
   auto fetch = [&](int tile, int chunk) {
     int b, x0, y0, z0;
     tile_origin(tile, b, x0, y0, z0);
+    if constexpr (NCX) {
+      fetch_ncx(b, x0 * KA(sx) - KA(px), y0 * KA(sy) - KA(py), z0 * KA(sz) - KA(pz), KA(IX), KA(IY), KA(IZ),
+                KA(in_c), KA(in_fmt));
+      return;
+    }
     const int IX = KA(IX), IY = KA(IY), IZ = KA(IZ), ICs = KA(ICs);
     const uint32_t bZ = (uint32_t)ICs * ES, bY = (uint32_t)IZ * bZ, bX = (uint32_t)IY * bY;
     const int gx0 = x0 * KA(sx) - KA(px), gy0 = y0 * KA(sy) - KA(py), gz0 = z0 * KA(sz) - KA(pz);
@@ -334,6 +393,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     a.fNTZ.divmod(r, r, tzi);
     a.fNTY.divmod(r, txi, tyi);
     const int x0 = txi * a.TX, y0 = tyi * a.TY, z0 = tzi * a.TZ;
+    if constexpr (NCX) {
+      fetch_ncx(b, x0 * a.sx - a.px, y0 * a.sy - a.py, z0 * a.sz - a.pz, a.IX, a.IY, a.IZ, a.in_c, a.in_fmt);
+      return;
+    }
     const int IX = a.IX, IY = a.IY, IZ = a.IZ, ICs = a.ICs;
     const uint32_t bZ = (uint32_t)ICs * ES, bY = (uint32_t)IZ * bZ, bX = (uint32_t)IY * bY;
     const int gx0 = x0 * a.sx - a.px, gy0 = y0 * a.sy - a.py, gz0 = z0 * a.sz - a.pz;
@@ -410,6 +473,45 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
         if (v < HV)
           *reinterpret_cast<uint4 *>(alds + v * CKP + cv * VEC) =
               activate(val[u], okv[u], chunk);
+      }
+    }
+  };
+
+  // NCX: pf -> E channels (0 past in_c and outside the input) into the halo
+  // image, and the channels-last copy of the voxels this tile owns: its output
+  // range, plus the kernel's overhang on the grid's last tile of each axis
+  auto ncx_store = [&](int b, int ox0, int oy0, int oz0) {
+    const int fmt = KA(in_fmt), INC = KA(in_c);
+    const bool lastx = ox0 + KA(TX) >= KA(OX), lasty = oy0 + KA(TY) >= KA(OY), lastz = oz0 + KA(TZ) >= KA(OZ);
+    E *const xo = reinterpret_cast<E *>(KA(xcl));
+    const int IX = KA(IX), IY = KA(IY), IZ = KA(IZ), ICs = KA(ICs);
+#pragma unroll
+    for (int u = 0; u < NPFR; ++u) {
+      const bool ok = (okbits >> u) & 1u;
+      float f[VEC];
+      const uint32_t r[4] = {pf[u].x, pf[u].y, pf[u].z, pf[u].w};
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        float x = 0.f;
+        if (j < 4) {
+          x = fmt == 1 ? __uint_as_float(r[j])
+                       : fmt == 2 ? (float)__builtin_bit_cast(_Float16, (uint16_t)r[j]) : __uint_as_float(r[j] << 16);
+        }
+        f[j] = (ok && j < INC) ? x : 0.f;
+      }
+      uint4 w;
+      if constexpr (ES == 2) {
+        w = pack8(f);
+      } else {
+        w = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+      }
+      const int hp = hpk[u];
+      *reinterpret_cast<uint4 *>(alds + (hp >= 0 ? (tid + u * VS) * CKP : HV * CKP)) = w;
+      const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
+      if (xo && ok && (hx < KA(TX) || lastx) && (hy < KA(TY) || lasty) && (hz < KA(TZ) || lastz)) {
+        const size_t vox = (((size_t)b * IX + ox0 * KA(sx) - KA(px) + hx) * IY + oy0 * KA(sy) - KA(py) + hy) * IZ +
+                           oz0 * KA(sz) - KA(pz) + hz;
+        *reinterpret_cast<uint4 *>(xo + vox * ICs) = w;
       }
     }
   };
@@ -590,10 +692,16 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
         for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
         lds_barrier();
+        if constexpr (NCX) {
+          int b, ox0, oy0, oz0;
+          tile_origin(tile, b, ox0, oy0, oz0);
+          ncx_store(b, ox0, oy0, oz0);
+        } else {
 #pragma unroll
         for (int u = 0; u < NPFR; ++u)   // every element is written (the waits stay exact)
           *reinterpret_cast<uint4 *>(alds + (hpk[u] >= 0 ? (tid / CV + u * VS) * CKP + cv * VEC : HV * CKP)) =
               activate(pf[u], (okbits >> u) & 1u, chunk);
+        }
         PH_MARK(0);
         if (wpre)
           wstore();
@@ -875,9 +983,19 @@ int launch_bconv_f32(const GConvArgs &a, hipStream_t s);
     switch (mode) {                                                                                  \
       BCONV_MODE(E_, TAG_, CV_, NS_, MP_, PF_, 0, "")                                                \
       BCONV_MODE(E_, TAG_, CV_, NS_, MP_, PF_, 1, ",bnb")                                            \
+      BCONV_NCX(E_, TAG_, CV_, NS_, MP_, PF_)                                                        \
     }                                                                                                \
     launched = true;                                                                                 \
   }
+// the NCXYZ first-layer instances (MODE 2): one channel group, prefetched halo
+#define BCONV_NCX(E_, TAG_, CV_, NS_, MP_, PF_) BCONV_NCX_##CV_(E_, TAG_, NS_, MP_, PF_)
+#define BCONV_NCX_2(E_, TAG_, NS_, MP_, PF_)
+#define BCONV_NCX_4(E_, TAG_, NS_, MP_, PF_)
+#define BCONV_NCX_1(E_, TAG_, NS_, MP_, PF_) BCONV_NCX1_PF##PF_(E_, TAG_, NS_, MP_)
+#define BCONV_NCX1_PF0(E_, TAG_, NS_, MP_)
+#define BCONV_NCX1_PF4(E_, TAG_, NS_, MP_) BCONV_MODE(E_, TAG_, 1, NS_, MP_, 4, 2, ",ncx")
+#define BCONV_NCX1_PF8(E_, TAG_, NS_, MP_) BCONV_MODE(E_, TAG_, 1, NS_, MP_, 8, 2, ",ncx")
+#define BCONV_NCX1_PF12(E_, TAG_, NS_, MP_) BCONV_MODE(E_, TAG_, 1, NS_, MP_, 12, 2, ",ncx")
 #define BCONV_PF(E_, TAG_, CV_, NS_, MP_)                                               \
   BCONV_CASE(E_, TAG_, CV_, NS_, MP_, 0) else BCONV_CASE(E_, TAG_, CV_, NS_, MP_, 4) else \
   BCONV_CASE(E_, TAG_, CV_, NS_, MP_, 8) else BCONV_CASE(E_, TAG_, CV_, NS_, MP_, 12)
@@ -898,7 +1016,7 @@ template <> bool bconv_launch_cv<uint16_t, 1>(const GConvArgs &, hipStream_t, co
 template <> bool bconv_launch_cv<uint16_t, 2>(const GConvArgs &, hipStream_t, const dim3 &, double, double);
 template <> bool bconv_launch_cv<uint16_t, 4>(const GConvArgs &, hipStream_t, const dim3 &, double, double);
 #define BCONV_CV_BODY(E_, TAG_, CV_)                                                                 \
-  const int mode = a.bn_y ? 1 : 0;                                                                   \
+  const int mode = a.bn_y ? 1 : a.in_fmt ? 2 : 0;                                                    \
   bool launched = false;                                                                             \
   BCONV_NS(E_, TAG_, CV_)                                                                            \
   return launched;
@@ -906,6 +1024,9 @@ template <> bool bconv_launch_cv<uint16_t, 4>(const GConvArgs &, hipStream_t, co
 // Launch of the planned variant (+ the K-split reduce) for element type E.
 #define BCONV_LAUNCH_BODY(E_, TAG_)                                                                  \
   const dim3 grid(a.gridx, a.CoutW / (a.NSUB * 16), a.ksplit);                                       \
+  if (a.in_fmt && (a.CK != BElem<E_>::VEC || a.NPF == 0 || a.bn_y || a.in_scale || a.ksplit > 1 ||    \
+                   a.nph > 1 || a.in_c < 1 || a.in_c > 4))                                            \
+    return fail(4, "bconv: NCXYZ input needs a first-layer forward (one channel group, prefetched)"); \
   if (grid.y > 65535 || grid.z > 65535) return fail(4, "bconv: grid too large");                     \
   if (a.ksplit > 1 && !a.partial) return fail(5, "bconv: K split needs a partial workspace");        \
   const double fl = a.flops > 0 ? a.flops                                                            \

@@ -224,6 +224,15 @@ struct GConvArgs {
   FastDiv fKZ, fKY;                   // tap index decomposition (conv8 K loop)
   int dbg;                            // ablation bits (HCU_CONV8_DBG; 0 in production)
   int HZr, MZ;                        // conv8: loaded halo z extent, z stride of the M rows
+  // The network input read in the caller's NCXYZ layout by the first layer's
+  // halo staging (no separate channels-last pass): in_fmt 1 / 2 / 3 = `in` is
+  // [B][in_c][IX][IY][IZ] fp32 / fp16 / bf16 (in_c <= 4 real channels, the
+  // rest of the ICs channels read 0); xcl != null: the staging also stores the
+  // channels-last copy [B][IX][IY][IZ][ICs] the weight gradient reads, each
+  // input voxel by exactly one tile; `w` is then the PyTorch-layout weight
+  // [Cout][in_c][KX*KY*KZ] (groups 1).  in_fmt 0: `in` is channels-last.
+  int in_fmt, in_c;
+  float *xcl;
   // dgrad epilogue fused with the BatchNorm+ReLU backward reduction of the
   // layer whose output this gradient is for (bn_y = its pre-BN y, same layout
   // as out): the stored value is dz = v * [y*scale+shift > 0] and the stats

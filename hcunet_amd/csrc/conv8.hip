@@ -44,11 +44,19 @@ bool conv8_disabled() {   // HCU_NO_CONV8=1 keeps the 16x16x4 kernels (A/B testi
 
 // BNB: input gradient with the fused BatchNorm backward (a.bn_y set); a
 // template parameter so its loads never share registers or waits with the
-// forward epilogue.  Launch constants used in the tile loop are read from an
+// forward epilogue.  INX (C4 == 1, forward): 0 = channels-last input; 1 / 2 /
+// 3 = the network input in its NCXYZ layout, fp32 / fp16 / bf16 (GConvArgs::
+// in_fmt): each halo element gathers its 4 channels from the channel planes
+// (consecutive lanes hold consecutive z, then y: 64 lanes read one contiguous
+// run of a plane), converts them to fp32 while writing the halo image, and
+// stores the channels-last copy of the voxels its tile owns (a.xcl); its
+// weights are the PyTorch-layout [Cout][in_c][T] (groups 1), not the packed
+// image.  Launch constants used in the tile loop are read from an
 // LDS copy of the arguments (kuni, common.h), so they do not pin scalar
 // registers for the whole kernel.
-template <int C4, int G, int NPF, bool BNB>
+template <int C4, int G, int NPF, bool BNB, int INX>
 __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
+  static_assert(INX == 0 || (C4 == 1 && !BNB), "NCXYZ input: first-layer forward only");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ __attribute__((aligned(16))) char sa_raw[sizeof(GConvArgs)];
   GConvArgs &sa = *reinterpret_cast<GConvArgs *>(sa_raw);
@@ -67,8 +75,17 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
 
-  for (int i = tid; i < T * C4 * 8; i += 256)
-    reinterpret_cast<float4 *>(wlds)[i] = reinterpret_cast<const float4 *>(a.w)[i];
+  if constexpr (INX > 0) {
+    // the first layer reads the PyTorch-layout weights [Cout][in_c][T]
+    // (groups == 1) itself, so it does not wait for the packed images
+    for (int i = tid; i < T * 32; i += 256) {
+      const int t = i >> 5, col = (i >> 2) & 7, j = i & 3;
+      wlds[i] = (col < a.Cout && j < a.in_c) ? a.w[((size_t)col * a.in_c + j) * T + t] : 0.f;
+    }
+  } else {
+    for (int i = tid; i < T * C4 * 8; i += 256)
+      reinterpret_cast<float4 *>(wlds)[i] = reinterpret_cast<const float4 *>(a.w)[i];
+  }
   for (int t = tid; t < T; t += 256) {
     const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
     toffs[t] = (kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz) * 4;
@@ -148,6 +165,13 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   // applied when the element is written to LDS, selected to 0 outside.
   floatx4 pf[NPF];
   uint32_t okbits = 0;
+  // NCXYZ input (INX > 0): the raw loaded values (fp32 bits, or a 16-bit
+  // value in the low half), converted when the halo image is written
+  auto cvt = [&](float raw) -> float {
+    if constexpr (INX == 2) return (float)__builtin_bit_cast(_Float16, (uint16_t)__float_as_uint(raw));
+    if constexpr (INX == 3) return __uint_as_float(__float_as_uint(raw) << 16);
+    return raw;
+  };
   auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
     int r, tzi, tyi, txi;
     sa.fNT.uni().divmod(tile, b, r);
@@ -161,6 +185,33 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   auto fetch = [&](int tile) {
     int b, ox0, oy0, oz0;
     tile_origin(tile, b, ox0, oy0, oz0);
+    if constexpr (INX > 0) {
+      constexpr int ES = INX == 1 ? 4 : 2;
+      const int IX = KA(IX), IY = KA(IY), IZ = KA(IZ), HZr = KA(HZr), INC = KA(in_c);
+      const int plane = IX * IY * IZ;
+      const char *bp = reinterpret_cast<const char *>(KA(in)) + (size_t)b * INC * plane * ES;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)bp, 0, INC * plane * ES, 0x00020000);
+      const int gx0 = ox0 - KA(px), gy0 = oy0 - KA(py), gz0 = oz0 - KA(pz);
+      okbits = 0;
+#pragma unroll
+      for (int u = 0; u < NPF; ++u) {
+        const int hp = hpk[u];
+        const int gx = gx0 + (hp >> 20), gy = gy0 + ((hp >> 10) & 1023), gz = gz0 + (hp & 1023);
+        const bool ok = (hp >= 0) & ((hp & 1023) < HZr) & ((unsigned)gx < (unsigned)IX) &
+                        ((unsigned)gy < (unsigned)IY) & ((unsigned)gz < (unsigned)IZ);
+        const int vo = (gx * IY + gy) * IZ + gz;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int off = (ok && c < INC) ? (c * plane + vo) * ES : 0x7ffffff0;
+          if constexpr (INX == 1)
+            pf[u][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+          else
+            pf[u][c] = __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
+        }
+        okbits |= (uint32_t)ok << u;
+      }
+      return;
+    }
     const int IX = KA(IX), IY = KA(IY), IZ = KA(IZ), ICs = KA(ICs), HZr = KA(HZr);
     const uint32_t bZ = (uint32_t)ICs * 4, bY = (uint32_t)IZ * bZ, bX = (uint32_t)IY * bY;
     const int gx0 = ox0 - KA(px), gy0 = oy0 - KA(py), gz0 = oz0 - KA(pz);
@@ -202,10 +253,27 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     int b, ox0, oy0, oz0;
     tile_origin(tile, b, ox0, oy0, oz0);
     lds_barrier();
+    // (NCXYZ input) the input voxels this tile owns in the channels-last copy:
+    // its output tile's x / y / z range, plus the kernel's overhang on the
+    // grid's last tile of each axis
+    const bool lastx = ox0 + KA(TX) >= KA(OX), lasty = oy0 + KA(TY) >= KA(OY), lastz = oz0 + KA(TZ) >= KA(OZ);
+    float *const xclp = INX > 0 ? KA(xcl) : nullptr;
 #pragma unroll
     for (int u = 0; u < NPF; ++u) {
       const int idx = tid + u * 256;
       floatx4 v = pf[u];
+      if constexpr (INX > 0) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = cvt(v[c]);
+        const int hp = hpk[u];
+        const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
+        if (xclp && ((okbits >> u) & 1u) && (hx < KA(TX) || lastx) && (hy < KA(TY) || lasty) &&
+            (hz < KA(TZ) || lastz)) {
+          const int IY = KA(IY), IZ = KA(IZ);
+          const size_t vox = (((size_t)b * KA(IX) + ox0 - KA(px) + hx) * IY + oy0 - KA(py) + hy) * IZ + oz0 - KA(pz) + hz;
+          *reinterpret_cast<floatx4 *>(xclp + vox * 4) = v;
+        }
+      }
       if (act) {
         v[0] = fmaxf(fmaf(v[0], sc.x, sh.x), 0.f);
         v[1] = fmaxf(fmaf(v[1], sc.y, sh.y), 0.f);
@@ -434,11 +502,23 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   if (C4 == C4_ && a.G8 == G_ && a.NPF == NPF_) {                                                \
     if (a.bn_y)                                                                                  \
       HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ",bnb>", fl, by,                       \
-                HCU_LAUNCH((conv8_kernel<C4_, G_, NPF_, true>), dim3(a.gridx), dim3(256), \
+                HCU_LAUNCH((conv8_kernel<C4_, G_, NPF_, true, 0>), dim3(a.gridx), dim3(256), \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
+    else if (C4_ == 1 && a.in_fmt == 1)                                                          \
+      HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ",ncx32>", fl, by,                     \
+                HCU_LAUNCH((conv8_kernel<1, G_, NPF_, false, 1>), dim3(a.gridx), dim3(256),      \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
+    else if (C4_ == 1 && a.in_fmt == 2)                                                          \
+      HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ",ncx16>", fl, by,                     \
+                HCU_LAUNCH((conv8_kernel<1, G_, NPF_, false, 2>), dim3(a.gridx), dim3(256),      \
+                                   a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
+    else if (C4_ == 1 && a.in_fmt == 3)                                                          \
+      HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ",ncxbf>", fl, by,                     \
+                HCU_LAUNCH((conv8_kernel<1, G_, NPF_, false, 3>), dim3(a.gridx), dim3(256),      \
                                    a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
     else                                                                                         \
       HCU_TIMED(s, "conv8_kernel<" #C4_ "," #G_ "," #NPF_ ">", fl, by,                           \
-                HCU_LAUNCH((conv8_kernel<C4_, G_, NPF_, false>), dim3(a.gridx), dim3(256), \
+                HCU_LAUNCH((conv8_kernel<C4_, G_, NPF_, false, 0>), dim3(a.gridx), dim3(256), \
                                    a.lds_bytes - (int)sizeof(GConvArgs), s, a));                 \
     launched = true;                                                                             \
   }
@@ -447,6 +527,8 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
 
 int launch_conv8(const GConvArgs &a, hipStream_t s) {
   const int C4 = a.ICs / 4;
+  if (a.in_fmt && (C4 != 1 || a.bn_y || a.in_scale || a.in_c < 1 || a.in_c > 4))
+    return fail(4, "conv8: NCXYZ input needs a first-layer forward with <= 4 channels");
   const double fl = a.flops > 0 ? a.flops
                                 : 2.0 * a.B * a.OX * a.OY * a.OZ * (double)a.Cout * a.KX * a.KY *
                                       a.KZ * a.ICs;

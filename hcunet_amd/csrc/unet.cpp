@@ -497,6 +497,10 @@ struct hcu_unet_plan {
   Dims xin;
   size_t xcl_off = 0;
   std::vector<ConvLayer> dc1, dc2, uc1, uc2;
+  // the first convolution stages the NCXYZ input itself (conv8, or bconv
+  // with one channel group; <= 4 input channels, groups 1): no channels-last
+  // layout pass, and its kernel reads t->x
+  bool ncx_first = false;
   std::vector<Dims> pooled;
   std::vector<size_t> pool_off;
   std::vector<ConvTLayer> up;
@@ -754,6 +758,14 @@ int build_plan(hcu_unet_plan &p) {
     cur = p.uc2[j].out;
   }
   if (p.Co > 4) return fail(HCU_ERR_UNSUPPORTED, "out_channels > 4 is not supported yet");
+  {
+    // HCU_NCX=0: the separate channels-last pass ahead of the first conv (A/B)
+    static const bool ncx_on = !(getenv("HCU_NCX") && getenv("HCU_NCX")[0] == '0');
+    const GConvArgs &f = p.dc1[0].fwd;
+    const bool conv8_ok = f.use_conv8 && f.ICs == 4 && p.es == 4;
+    const bool bconv_ok = f.use_bconv && f.CK == (p.es == 2 ? 8 : 4) && f.NPF > 0 && f.ksplit == 1 && f.nph <= 1;
+    p.ncx_first = ncx_on && s.in_channels <= 4 && s.g1 == 1 && (conv8_ok || bconv_ok);
+  }
   p.outd = mkdims(p.B, cur.X, cur.Y, cur.Z, p.Co, 4);
   {
     const int R = outconv_bwd_rows(cur.vox(), cur.Cs);
@@ -977,15 +989,22 @@ void tag(const std::string &layer, const char *phase) {
   if (timing_on()) timing_set_tag((layer + "." + phase).c_str());
 }
 
+// in_fmt > 0 (the first layer, hcu_unet_plan::ncx_first): `in` is the
+// caller's NCXYZ input volume, read by the conv's own halo staging, which also
+// writes the channels-last copy xcl_out (when not null).
 int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float *isc,
-                 const float *ish, int training) {
+                 const float *ish, int training, int in_fmt = 0, float *xcl_out = nullptr) {
   HCU_HIP(hipGetLastError());
   tag(L.name, "fwd");
   GConvArgs a = L.fwd;
   a.in = in;
+  a.in_fmt = in_fmt;
+  a.in_c = in_fmt ? L.in.C : 0;
+  a.xcl = xcl_out;
+  if (in_fmt) a.w = c.P + L.w_off;   // (read in the PyTorch layout by the NCXYZ staging)
   a.in_scale = isc;
   a.in_shift = ish;
-  a.w = c.fptr(c.sv, L.wf_off);
+  if (!in_fmt) a.w = c.fptr(c.sv, L.wf_off);
   a.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
   a.out = c.fptr(c.sv, L.y_off);
   a.stats = training ? c.part() : nullptr;
@@ -1307,18 +1326,33 @@ int hcu_unet_plan_bn_layers(const hcu_unet_plan *p, hcu_bn_layer_info *out, int 
 int ensure_side(const hcu_unet_plan &p, int dev);
 bool side_enabled();
 
+// part: 0 = the whole forward; 1 = its head (the input's channels-last
+// layout, or with ncx_first the first convolution reading the NCXYZ input
+// itself, and its BatchNorm finalize): the launches that read t->x, issued
+// directly ahead of a replayed graph of part 2 = the rest, so a new input
+// tensor every step (a data loader) does not key a new graph.
 static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training,
-                           hipStream_t stream, bool input_done = false, bool split = false) {
+                           hipStream_t stream, int part = 0, bool split = false) {
   Ctx c{p, *t, (hipStream_t)stream, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   c.split = split;
   c.ws = split ? p.side : c.s;
   const hcu_unet_spec &s = p.spec;
   float *xcl = c.fptr(c.sv, p.xcl_off);
-  tag(std::string("in"), "fwd");
-  if (!input_done)
-    if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
-                             t->x_dtype))
-      return e;
+  if (part != 2) {
+    tag(std::string("in"), "fwd");
+    if (!p.ncx_first) {
+      if (int e = launch_to_cl(t->x, xcl, p.B, p.xin.C, p.xin.Cs, p.xin.vox() / p.B, c.s, c.bf(),
+                               t->x_dtype))
+        return e;
+    } else {
+      // NCXYZ input staged by the first conv; the channels-last copy only
+      // where a backward will read it
+      const int fmt = t->x_dtype == HCU_F16 ? 2 : t->x_dtype == HCU_BF16 ? 3 : 1;
+      float *xo = (p.flags & HCU_PLAN_FORWARD_ONLY) ? nullptr : xcl;
+      if (int e = conv_forward(c, p.dc1[0], t->x, nullptr, nullptr, training, fmt, xo)) return e;
+    }
+    if (part == 1) return HCU_OK;
+  }
   tag(std::string("prep"), "fwd");
   // training forwards lay out the input-gradient weight images too; laying
   // them out on the backward's branch instead measured equal on config 3 and
@@ -1358,7 +1392,8 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   for (int i = 0; i < p.L; ++i) {
     const ConvLayer &c1 = p.dc1[i], &c2 = p.dc2[i];
     if (i == 1 && ev_rest) HCU_HIP(hipStreamWaitEvent(c.s, ev_rest, 0));
-    if (int e = conv_forward(c, c1, src, ssc, ssh, training)) return e;
+    if (!(i == 0 && p.ncx_first))   // (else: run in the head)
+      if (int e = conv_forward(c, c1, src, ssc, ssh, training)) return e;
     const BNCoef b1 = coef_at(c.sv, c1.bn);
     if (int e = conv_forward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, training)) return e;
     const BNCoef b2 = coef_at(c.sv, c2.bn);
@@ -1457,17 +1492,14 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
     if (int e = ensure_side(p, dev)) return e;
   }
   if (graphs_for(p, false) && !timing_on()) {
-    tag(std::string("in"), "fwd");
-    if (int e = launch_to_cl(t->x, reinterpret_cast<float *>((char *)t->saved + p.xcl_off), p.B, p.xin.C,
-                             p.xin.Cs, p.xin.vox() / p.B, (hipStream_t)stream, p.es == 2, t->x_dtype))
-      return e;
+    if (int e = enqueue_forward(p, t, training, (hipStream_t)stream, 1, split)) return e;
     std::vector<uintptr_t> key = {0, (uintptr_t)t->out, (uintptr_t)t->params, (uintptr_t)t->saved,
                                   (uintptr_t)t->scratch, (uintptr_t)training, (uintptr_t)split};
     append_bn_key(key, p, t);
     return run_graphed(p, key, (hipStream_t)stream,
-                       [&](hipStream_t s) { return enqueue_forward(p, t, training, s, true, split); });
+                       [&](hipStream_t s) { return enqueue_forward(p, t, training, s, 2, split); });
   }
-  return enqueue_forward(p, t, training, (hipStream_t)stream, false, split);
+  return enqueue_forward(p, t, training, (hipStream_t)stream, 0, split);
 }
 
 static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout,

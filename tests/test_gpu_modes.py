@@ -28,6 +28,7 @@ kw = %(kw)s
 torch.manual_seed(0)
 m = Unet_Constructor(**kw).cuda().train()
 x = torch.from_numpy(inputs.make_x(%(shape)r)).cuda()
+x = x.to({'f16': torch.float16, 'bf16': torch.bfloat16}.get(os.environ.get('HCU_TEST_XDT'), torch.float32))
 res = []
 for it in range(3):          # 3 steps: the graphed mode replays its capture
     for p in m.parameters():
@@ -209,3 +210,21 @@ def test_kernel_family_switches_match_default(tmp_path, bf16):
                     bad.append((key, it, names[k], r, rel))
                 worst[key] = max(worst.get(key, 0.0), r)
     assert not bad, (bad[:8], {k: '%.2e' % v for k, v in worst.items()})
+
+
+@pytest.mark.parametrize('bf16,xdt', [('0', 'f32'), ('1', 'f32'), ('1', 'f16'), ('1', 'bf16')])
+def test_ncxyz_first_layer_matches_layout_pass(tmp_path, bf16, xdt):
+    """The first convolution staging the caller's NCXYZ volume itself (fp32,
+    fp16 or bf16; conv8 / bconv NCXYZ instances, weights in their PyTorch
+    layout, the channels-last copy for the weight gradient written by the
+    tiles that own each voxel) against the separate channels-last pass
+    (HCU_NCX=0): outputs and every gradient bitwise equal over 3 steps (the
+    same converted values reach the same MFMAs), the graphed forward
+    included."""
+    kw = KW if bf16 == '0' else KW.replace('[8, 16, 32, 64, 128]', '[16, 32, 64, 128]')
+    env = {'HCU_TEST_BF16': bf16, 'HCU_TEST_XDT': xdt}
+    a = _run(tmp_path, 'lay' + bf16 + xdt, dict(env, HCU_NCX='0'), kw=kw)
+    b = _run(tmp_path, 'ncx' + bf16 + xdt, env, kw=kw)
+    bad = [(it, k, (x - y).abs().max().item())
+           for it in range(3) for k, (x, y) in enumerate(zip(a[it], b[it])) if not torch.equal(x, y)]
+    assert not bad, bad[:8]
