@@ -263,7 +263,9 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
     if (NSUB > 1 && nb16 < NSUB && !(NSUB == 2 && nb16 >= 2)) continue;
     if (NSUB == 4 && nb16 < 4) continue;
     if (NSUB == 2 && nb16 < 2) continue;
-    if (a.nph > 1 && (a.Cout % (NSUB * 16) || a.Cout % 8)) continue;
+    // (phases folded into N: a lane's 4 columns share a phase; bf16 stores 8
+    // channels per 16 bytes of the packed weights)
+    if (a.nph > 1 && (a.Cout % (a.bes == 2 ? 8 : 4))) continue;
     const int NT = NSUB * 16;
     const int CoutW = round_up(Nlog, NT);
     const int nN = CoutW / NT;

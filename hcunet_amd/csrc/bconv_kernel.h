@@ -229,9 +229,26 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     }
     toffs[e] = off * CKP + ((e & 3) % CV) * VEC;
   }
-  // first stored channel of the block (ConvTranspose3d phases: all NT columns
-  // of a block belong to one phase, the planner requires Cout % NT == 0)
+  // first stored channel of the block (ConvTranspose3d phases folded into N:
+  // column n0 + j is channel (n0 + j) % Cout of phase (n0 + j) / Cout)
   const int co0 = a.nph > 1 ? n0 - (n0 / a.Cout) * a.Cout : n0;
+  // the 4 stored columns of lane group g in column subtile n: their first
+  // channel (-1: past the stored channels) and the output offset of their
+  // phase (Cout % 4 == 0, so the 4 share it; a block may span phases)
+  int cn[NSUB], qo[NSUB];
+#pragma unroll
+  for (int n = 0; n < NSUB; ++n) {
+    const int gcl = n0 + n * 16 + g * 4;
+    if (a.nph > 1) {
+      const int ph = gcl / a.Cout;
+      const int qz = ph % a.phz, qy = (ph / a.phz) % a.phy, qx = ph / (a.phz * a.phy);
+      cn[n] = ph < a.nph ? gcl - ph * a.Cout : -1;
+      qo[n] = ((qx * a.SY + qy) * a.SZ + qz) * a.OCs;
+    } else {
+      cn[n] = gcl < a.OCs ? gcl : -1;
+      qo[n] = 0;
+    }
+  }
   // (the coefficient loads follow the first halo fetch: load_coefs below)
 
   auto tile_origin = [&](int tile, int &b, int &ox0, int &oy0, int &oz0) {
@@ -420,7 +437,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   };
   auto load_coefs = [&]() {
     for (int j = tid; j < NT; j += 256) {
-      const int c = co0 + j;
+      const int c = a.nph > 1 ? (n0 + j) % a.Cout : n0 + j;
       coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
       const bool bn = BNB && !split && c < a.OCs;
       coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;
@@ -562,18 +579,11 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // wave stores (its value + bias), see below
   bool need_piv = true;
   auto epilogue = [&](int b, int ox0, int oy0, int oz0) {
-    int qx = 0, qy = 0, qz = 0;
-    if (KA(nph) > 1) {
-      const int ph = blockIdx.y * NT / KA(Cout), phz = KA(phz), phy = KA(phy);
-      qz = ph % phz;
-      qy = (ph / phz) % phy;
-      qx = ph / (phz * phy);
-    }
     const int OX = KA(OX), OY = KA(OY), OZ = KA(OZ), OCs = KA(OCs);
     const bool interior = ox0 + KA(TX) <= OX && oy0 + KA(TY) <= OY && oz0 + KA(TZ) <= OZ;
     const int sample = KA(SX) * KA(SY) * KA(SZ) * OCs;
-    const int tb = (((ox0 * KA(osx) + KA(ofx) + qx) * KA(SY) + oy0 * KA(osy) + KA(ofy) + qy) * KA(SZ) +
-                    oz0 * KA(osz) + KA(ofz) + qz) * OCs + co0;
+    const int tb = (((ox0 * KA(osx) + KA(ofx)) * KA(SY) + oy0 * KA(osy) + KA(ofy)) * KA(SZ) +
+                    oz0 * KA(osz) + KA(ofz)) * OCs;
     const size_t sb = (size_t)b * sample;
     const int es = split ? 4 : ES;
     void *obase = split ? (void *)(KA(partial) + (size_t)blockIdx.z * KA(slice_floats) + sb)
@@ -598,9 +608,8 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       if (BNB)
 #pragma unroll
         for (int n = 0; n < NSUB; ++n) {
-          const int col = n * 16 + g * 4;
-          const bool ok = vok & (co0 + col < OCs);
-          yv[n] = bload4(tag, yrs, ok ? (rof + col) * ES : 0x3ffffff0);
+          const bool ok = vok & (cn[n] >= 0);
+          yv[n] = bload4(tag, yrs, ok ? (rof + qo[n] + cn[n]) * ES : 0x3ffffff0);
         }
       if (fwdstat && need_piv) {
         // the wave's pivot: the lowest valid voxel of this M-subtile (lanes
@@ -623,8 +632,8 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #pragma unroll
       for (int n = 0; n < NSUB; ++n) {
         const int col = n * 16 + g * 4;
-        const bool ok = vok & (co0 + col < OCs);
-        const int off = ok ? rof + col : 0x1fffffff;
+        const bool ok = vok & (cn[n] >= 0);
+        const int off = ok ? rof + qo[n] + cn[n] : 0x1fffffff;
         floatx4 v = acc[j][n];
         if (split) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ors, off * 4, 0, 0);

@@ -391,6 +391,7 @@ struct WGradFinalize {
   float *dw, *db;
   int KB, Mtot, Ntot, T;
   int mode;   // 0 Conv3d (taps rows), 1 ConvTranspose3d, 2 bias column sums (db[c < Cout]),
+              // 4 the same from forward-statistics rows [KB][Ntot] of {S1, S2, K, n} (S1 + n*K),
               // 3 ConvTranspose3d in the phase form (WGradArgs::nph): row (j, ci), column
               // (q, co) -> dW[ci][co][t], t = (J-1-j)*S + q per dimension; db[co] = sum_q bias row
   int Cout, Cin_g, groups, fold_mod, ACs;   // conv

@@ -124,7 +124,7 @@ struct ConvTLayer {
   GConvArgs dgrad{};
   WGradArgs wg{};
   // the weight gradient of the phase-folded forward (WGradArgs::nph: phases
-  // as extra columns, the bias from its ones row -- no chansum), fp32 U-Net
+  // as extra columns; the bias from the column-sum rows of dU), fp32 U-Net
   // decoders with kernel % stride == 0 and Cout % 4 == 0
   WGradArgs wgp{};
   bool wg_phase = false;
@@ -452,8 +452,9 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
   }
   u.wg_phase = false;
   // The weight gradient of the phase-folded forward (stride phases as extra
-  // output columns) on wgrad3, its bias from chansum; the other layers run the
-  // per-tap wgrad_kernel + chansum.
+  // output columns) on wgrad3; the other layers run the per-tap wgrad_kernel.
+  // (The U-Net's bias gradient: the column sums of dU, written by the
+  // folded conv1's input-gradient kernel; layer chains: chansum.)
   if (!bf && u.fused && o % 4 == 0) {
     // dW'[(j, ci)][(q, co)] = sum_o A[o + j - (J-1)][ci] * dU[o*S + q][co] over the
     // phase grid o (the forward's fused GEMM, hcat/unet.py:294-298)
@@ -525,6 +526,9 @@ struct hcu_unet_plan {
   int nbuf = HCU_NBUF_RING;
   bool no_reuse = false;
   size_t part_off = 0, wpart_off = 0, wprep_off = 0, kpart_off = 0;
+  // per decoder level: the column-sum rows of dU (the up_conv bias gradient)
+  // written by the folded conv1's input-gradient kernel
+  size_t colsum_off[HCU_MAX_LEVELS] = {};
   double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
   // Layer-chain plans (hcu_chain_*): a sequence of ops instead of the U-Net.
   struct ChainOp {
@@ -858,6 +862,8 @@ int build_plan(hcu_unet_plan &p) {
   p.wpart_off = scratch.take_floats(p.wpart_floats);
   p.wprep_off = scratch.take_floats(fwd_only ? 0 : p.max_wprep);
   p.kpart_off = scratch.take_floats(std::max<size_t>(p.max_kpart, 1));
+  for (int j = 0; j + 1 < L; ++j)
+    p.colsum_off[j] = scratch.take_floats(fwd_only ? 0 : (size_t)gconv_rows(p.uc1[j].dgrad) * p.uc1[j].dgrad.CoutW * 4);
   p.scratch_bytes = scratch.off;
   if (getenv("HCU_PLAN_LOG")) {   // weight-gradient kernels and their partial slabs (measurement)
     auto wlog = [](const std::string &n, const WGradArgs &w) {
@@ -1052,9 +1058,14 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 // Weight/bias gradient and (optionally) input gradient of one Conv3d layer.
 // dy holds dY of L.  With `bnl`, the input gradient leaves as dz of layer bnl
 // (its BatchNorm+ReLU backward fused into the dgrad) and *bn_done is set.
+// With `colsum` (and no bnl) the input gradient's kernel also writes its
+// per-workgroup statistics rows there (gconv_rows x CoutW of {S1, S2, K, n}):
+// the column sums of dA, finalized as the bias gradient of the layer that
+// produced A (a ConvTranspose3d: no separate reduction pass over dA).
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
-                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr) {
+                  const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr,
+                  float *colsum = nullptr) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
   WGradArgs w = L.wg;
@@ -1091,6 +1102,7 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   a.out = dA;
   a.partial = c.kpart();
   const bool fused = fuse_bnbwd(c, a, bnl);
+  if (!fused && colsum) a.stats = colsum;
   if (int e = launch_conv_any(a, c.s)) return e;
   if (!fused) return 0;
   tag(bnl->name, "bnbwd");
@@ -1482,7 +1494,11 @@ int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int t
   // runs: config 3 (11.6 M parameters) 6.418-6.434 vs 6.448-6.453 ms/step;
   // config 2 (0.7 M, ~23 us of re-layout) 2.103-2.129 vs 2.058-2.071: there
   // the branch's kernels slow level 0 more than the overlap returns.
-  const bool split = p.n_params >= (int64_t)4 << 20 && training && side_enabled() && !timing_on() &&
+  // (HCU_SPLIT_FWD_PARAMS: the parameter count from which the split applies;
+  // tests lower it to run the split on a small network)
+  static const int64_t split_min = getenv("HCU_SPLIT_FWD_PARAMS") ? atoll(getenv("HCU_SPLIT_FWD_PARAMS"))
+                                                                  : (int64_t)4 << 20;
+  const bool split = p.n_params >= split_min && training && side_enabled() && !timing_on() &&
                      p.prep_fwd.size() > 2;
   std::unique_lock<std::mutex> lk(p.smu, std::defer_lock);
   if (split) {
@@ -1553,32 +1569,35 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       return e;
     if (!done1)
       if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
-    // conv1 (folded cat): dU into a fresh slot
+    // conv1 (folded cat): dU into a fresh slot; its input-gradient kernel also
+    // writes the column-sum rows of dU, the up_conv bias gradient
     if (int e = c.alloc(su)) return e;
     float *dU = c.buf(su);
-    if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, sb, dU, accumulate)) return e;
+    const int cs_rows = gconv_rows(c1.dgrad), cs_w = c1.dgrad.CoutW;
+    // (its own scratch region per level: written by the chain, read by the
+    // deferred finalize on the branch -- never a recycled slab of the arena,
+    // whose previous readers run on the branch)
+    float *csr = c.fptr(c.sc, p.colsum_off[j]);
+    if (int e = conv_backward(c, c1, U, nullptr, nullptr, Bf, sb, dU, accumulate, nullptr, training, nullptr, csr))
+      return e;
     // up_conv: bias and weight gradients on the branch, input gradient on the chain
     const ConvLayer &prev = j == 0 ? p.dc2[p.L - 1] : p.uc2[j - 1];
     const BNCoef bp = coef_at(c.sv, prev.bn);
     tag(u.name, "wgrad");
     if (int e = c.fork()) return e;
-    if (u.wg_phase) {   // the weight gradient in one launch (WGradArgs::nph), bias with it or from chansum
-      if (!u.wgp.bias_row) {
-        const int R = chansum_rows(u.out.vox(), u.out.Cs);
-        float *cs = nullptr;
-        if (int e = c.slab((size_t)R * u.out.Cs, cs)) return e;
-        if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, cs, R, c.wstream(), c.bf())) return e;
-        WGradFinalize fb{};
-        fb.partial = cs;
-        fb.db = c.G + u.b_off;
-        fb.KB = R;
-        fb.Mtot = 1;
-        fb.Ntot = u.out.Cs;
-        fb.mode = 2;
-        fb.Cout = u.Cout;
-        fb.accumulate = accumulate;
-        if (int e = c.pend_wgf(fb)) return e;
-      }
+    {
+      WGradFinalize fb{};   // the bias: column sums of dU, with the batched finalizes
+      fb.partial = csr;
+      fb.db = c.G + u.b_off;
+      fb.KB = cs_rows;
+      fb.Mtot = 1;
+      fb.Ntot = cs_w;
+      fb.mode = 4;
+      fb.Cout = u.Cout;
+      fb.accumulate = accumulate;
+      if (int e = c.pend_wgf(fb)) return e;
+    }
+    if (u.wg_phase) {   // the weight gradient in one launch (WGradArgs::nph, wgrad3)
       WGradArgs w = u.wgp;
       w.A = c.fptr(c.sv, prev.y_off);
       w.a_scale = bp.scale;
@@ -1589,7 +1608,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       WGradFinalize f{};
       f.partial = w.partial;
       f.dw = c.G + u.w_off;
-      f.db = w.bias_row ? c.G + u.b_off : nullptr;
+      f.db = nullptr;
       f.KB = w.KB;
       f.Mtot = w.Mtot;
       f.Ntot = w.Ntot;
@@ -1606,24 +1625,6 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       f.accumulate = accumulate;
       if (int e = c.pend_wgf(f)) return e;
     } else {
-    {
-      const int R = chansum_rows(u.out.vox(), u.out.Cs);
-      float *cs = nullptr;
-      if (int e = c.slab((size_t)R * u.out.Cs, cs)) return e;
-      if (int e = launch_chansum(dU, u.out.vox(), u.out.Cs, cs, R, c.wstream(), c.bf()))
-        return e;
-      WGradFinalize fb{};   // the bias: column sums of the R rows, with the batched finalizes
-      fb.partial = cs;
-      fb.db = c.G + u.b_off;
-      fb.KB = R;
-      fb.Mtot = 1;
-      fb.Ntot = u.out.Cs;
-      fb.mode = 2;
-      fb.Cout = u.Cout;
-      fb.accumulate = accumulate;
-      if (int e = c.pend_wgf(fb)) return e;
-    }
-    {
       WGradArgs w = u.wg;
       w.A = c.fptr(c.sv, prev.y_off);
       w.a_scale = bp.scale;
@@ -1645,7 +1646,6 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       f.GCs = w.GCs;
       f.accumulate = accumulate;
       if (int e = c.pend_wgf(f)) return e;
-    }
     }
     if (int e = c.read_done(su)) return e;
     tag(u.name, "dgrad");
@@ -2125,7 +2125,9 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
         o.xs_off = saved.take_floats(L.sub_in.floats());
         p.max_sub = std::max({p.max_sub, L.sub_in.floats(), L.sub_out.floats()});
       }
-      L.y_off = saved.take_floats(L.out.floats());
+      // (out_cl: the last conv writes the caller's tensor and, without a
+      // BatchNorm, its backward never reads y: no saved buffer)
+      L.y_off = p.out_cl && i + 1 == cs.n_ops ? 0 : saved.take_floats(L.out.floats());
       if (o.bn_relu) {
         L.bn.coef_off = saved.take_floats((size_t)6 * L.bn.Cs);
         L.bn.gamma = s.gamma_off;

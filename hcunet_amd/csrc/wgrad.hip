@@ -740,7 +740,14 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
   const int tid = threadIdx.x, el = tid % EPB, sl = tid / EPB;
   const int64_t idx = (int64_t)blockIdx.x * EPB + el;
   double acc = 0.0;
-  if (idx < n) {
+  if (idx < n && f.mode == 4) {
+    // column sums from forward-statistics rows {S1, S2, K, n}: sum = S1 + n*K
+    const float4 *src = reinterpret_cast<const float4 *>(f.partial) + idx;
+    for (int k = sl; k < f.KB; k += S) {
+      const float4 r = src[(size_t)k * n];
+      acc += (double)r.x + (double)r.w * (double)r.z;
+    }
+  } else if (idx < n) {
     const float *src = f.partial + idx;
 #pragma unroll 4
     for (int k = sl; k < f.KB; k += S) acc += (double)src[(size_t)k * n];
@@ -783,7 +790,7 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
     *dst = f.accumulate ? *dst + v : v;
     return;
   }
-  if (f.mode == 2) {   // column sums of R rows (ConvTranspose bias: rows = chansum partials)
+  if (f.mode == 2 || f.mode == 4) {   // column sums of R rows (ConvTranspose bias)
     if (gcol < f.Cout && f.db) f.db[gcol] = f.accumulate ? f.db[gcol] + v : v;
     return;
   }

@@ -85,16 +85,11 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
     const int c = n * 16 + r16;
     goff[n] = ((c < CKG && co0 + c < a.Ntot) ? c * RSG : CKG * RSG) + kq;
   }
-  // ConvTranspose3d phase form (WGradArgs::nph): the block's columns lie in
-  // one stride phase q; G is read at o*S + q, channel co0 - q*GCout
-  int gq[3] = {0, 0, 0}, gcb = co0;
-  if (a.nph > 1) {
-    const int q = co0 / a.GCout;
-    gcb = co0 - q * a.GCout;
-    gq[2] = q % a.phz;
-    gq[1] = (q / a.phz) % a.phy;
-    gq[0] = q / (a.phz * a.phy);
-  }
+  // ConvTranspose3d phase form (WGradArgs::nph): column c is channel c % GCout
+  // of stride phase q = c / GCout, whose G is read at o*S + q.  A thread
+  // always stages the same 4-column group (below), whose 4 columns share a
+  // phase (GCout % 4 == 0): a block's columns may span phases.
+  int gq[3] = {0, 0, 0};
   floatx4 acc[MS][NS], accb[NS];
 #pragma unroll
   for (int m = 0; m < MS; ++m)
@@ -109,7 +104,15 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(const WGradArgs a) {
   // element -> (voxel, group) split is a shift; a thread always stages the
   // same 4-channel group (256 % CA4 == 0, 256 % CG4 == 0)
   const int lgA = __builtin_ctz(CKA / 4), lgG = __builtin_ctz(CKG / 4);
-  const int ca = ci0 + (tid & ((1 << lgA) - 1)) * 4, cg = gcb + (tid & ((1 << lgG) - 1)) * 4;
+  int cg = co0 + (tid & ((1 << lgG) - 1)) * 4;
+  if (a.nph > 1) {
+    const int q = cg / a.GCout;
+    cg -= q * a.GCout;
+    gq[2] = q % a.phz;
+    gq[1] = (q / a.phz) % a.phy;
+    gq[0] = q / (a.phz * a.phy);
+  }
+  const int ca = ci0 + (tid & ((1 << lgA) - 1)) * 4;
   const int rowa = (tid & ((1 << lgA) - 1)) * 4 * RSA, rowg = (tid & ((1 << lgG) - 1)) * 4 * RSG;
   const bool cok_a = ca < a.ACs, cok_g = cg < a.GCs && co0 + (tid & ((1 << lgG) - 1)) * 4 < a.Ntot;
   float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -299,7 +302,9 @@ int plan_wgrad3(WGradArgs &a) {
   if (ph && a.bias_row) return 1;   // (its bias comes from chansum)
   // (16-channel inputs stay on wgrad2: d2.c1 of config 2 ran 65 us here
   // against 52 us there; every wider layer measured faster here)
-  if (a.ACs % 32) return 1;
+  // (the ConvTranspose3d phase form also takes 16-channel inputs: the per-tap
+  // wgrad_kernel is its alternative)
+  if (a.ACs % (ph ? 16 : 32)) return 1;
   // 32-bit buffer offsets within one sample
   if ((double)a.AX * a.AY * a.AZ * a.ACs >= (double)(1 << 29) || (double)a.GX * a.GY * a.GZ * a.GCs >= (double)(1 << 29))
     return 1;
@@ -307,15 +312,21 @@ int plan_wgrad3(WGradArgs &a) {
   const int ntz = cdiv(a.PZ, 16), TZ = cdiv(a.PZ, ntz), TZP = round_up(TZ, 4);
   const int HAZP = TZP + (a.KZ - 1) * a.adz;
   const int ncols = ph ? a.nph * a.GCout : a.GCs;
-  const int cw = ph ? a.GCout : a.GCs;   // a column chunk stays inside one phase
-  if (cw % 32) return 1;
-  const int NS = cw % 64 == 0 ? 4 : 2;
+  // (phase form: a column chunk may span phases, a 4-column group may not)
+  if (ncols % 32 || (ph && a.GCout % 4)) return 1;
+  const int NS = ncols % 64 == 0 ? 4 : 2;
   const int CKG = NS * 16;
   const int nco = ncols / CKG;
   // Grid sized for 192 CUs: the weight-gradient branch overlaps the chain stream
   // (config 2 A/B, 3 reps: 192 -> 2.038-2.051, 176 -> 2.062-2.081, 208 -> 2.084-2.098,
   // 160 -> 2.083-2.090, side_cus() 224 -> 2.113-2.126 ms/step).
-  const int cus = 192;
+  // The small ConvTranspose3d layers (fewer than 32 output channels: u2.up /
+  // u3.up of config 2, 0.2 GFLOP) on 64 CUs: their few tiles spread over 192
+  // only take CUs from the chain (interleaved A/B, 3 runs: 1.998-2.002 ms per
+  // config-2 step at 64, 2.014-2.020 at 32, 2.025-2.028 at 128, 2.024-2.031
+  // at 192; the per-tap wgrad_kernel + chansum 2.017-2.019; a FLOP-
+  // proportional grid for every wgrad3 layer measured equal).
+  const int cus = ph && a.GCout < 32 ? 64 : 192;
   const int mss[3] = {9, 5, 3};
   const int ckas[3] = {64, 32, 16};
   const int txys[4][2] = {{4, 4}, {4, 2}, {2, 4}, {2, 2}};

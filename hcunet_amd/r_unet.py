@@ -407,12 +407,19 @@ class RDCNet(nn.Module):
                for i, c in enumerate((sd.conv1, sd.conv2, sd.conv3, sd.conv4, sd.conv5))]
         mix = _chain(sd, self, 'out_cl', sd.out_conv.in_channels, [('conv', sd.out_conv, None, False)],
                      in_part=C, **cl)
-        y = torch.zeros_like(x)
+        # The residual state y stays fp32, as the reference's under autocast
+        # (r_unet.py:223-225: fp32 zeros, and bf16 block output + fp32 y
+        # promotes to fp32); it is rounded to the compute dtype only where it
+        # enters a convolution (the cat of :223, out_conv of :226).
+        y = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+        trace = getattr(self, '_y_trace', None)   # (tests: y after every recurrence step)
         for t in range(10):
-            h = step(torch.cat((x, y), dim=-1), tr, bf16)
+            h = step(torch.cat((x, y.to(x.dtype)), dim=-1), tr, bf16)
             y = mix(torch.cat([d(h, tr, bf16) for d in dil], dim=-1), tr, bf16) + y
+            if trace is not None:
+                trace.append(y.detach().clone())
         y = _chain(self, self, 'out_cl', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],
-                   in_cl=True)(y, tr, bf16)
+                   in_cl=True)(y.to(x.dtype), tr, bf16)
         # 5 output channels: no bf16 phase-folded ConvTranspose3d tiling; fp32
         return _chain(self, self, 'convt', self.transposed_conv.in_channels,
                       [('convt', self.transposed_conv)])(y, tr, False)

@@ -78,6 +78,21 @@ def test_split_graphed_equals_serial(tmp_path):
             assert torch.equal(a, d)
 
 
+@pytest.mark.parametrize('bf16', ['0', '1'])
+def test_split_forward_equals_serial(tmp_path, bf16):
+    """The split training forward (the deeper levels' weight images laid out
+    on the branch stream while level 0 runs, the chain waiting before level 1;
+    the default from 4 M parameters) forced onto this small network
+    (HCU_SPLIT_FWD_PARAMS=0) against the serial run (HCU_SIDE=0): outputs and
+    gradients bitwise equal over 3 steps, fp32 and bf16."""
+    kw = KW if bf16 == '0' else KW.replace('[8, 16, 32, 64, 128]', '[16, 32, 64, 128]')
+    serial = _run(tmp_path, 'ser' + bf16, {'HCU_SIDE': '0', 'HCU_TEST_BF16': bf16}, kw=kw)
+    split = _run(tmp_path, 'spl' + bf16, {'HCU_SPLIT_FWD_PARAMS': '0', 'HCU_TEST_BF16': bf16}, kw=kw)
+    for it in range(3):
+        for k, (a, b) in enumerate(zip(serial[it], split[it])):
+            assert torch.equal(a, b), (it, k)
+
+
 def test_bf16_steps_are_deterministic(tmp_path):
     """Two processes running the same bf16 autocast training steps (split
     streams, graphed forward: the default) give bitwise-identical outputs and

@@ -274,3 +274,31 @@ def _train_step_with(net, g, x, mask, pwl):
     loss.backward()
     torch.cuda.synchronize()
     return out.detach().cpu(), float(loss.item())
+
+
+def test_rdcnet_bf16_residual_error_does_not_compound_512x512x24():
+    """BASELINE config 5's tile (512x512x24) under bf16 autocast: the
+    recurrence's residual state y stays fp32 (r_unet.py:223-225 under
+    autocast: fp32 zeros + bf16 block output -> fp32), so its distance to the
+    fp32 run (this build's fp32 path, pinned to the oracle at this tile by
+    test_rdcnet_full_tile_512x512x24_matches_oracle) after each of the 10
+    steps stays at the level of one bf16 block evaluation instead of adding a
+    bf16 rounding of the state every step: relative L2 of y_t <= 2e-2 for
+    every t, and y_10's error within 3x of y_1's."""
+    torch.manual_seed(0)
+    net = RDCNet(4, 5).cuda().train()
+    x = torch.from_numpy(inputs.make_x((1, 4, 512, 512, 24))).cuda()
+    traces = {}
+    for bf16 in (False, True):
+        net._y_trace = []
+        with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16, enabled=bf16):
+            net(x)
+        traces[bf16] = net._y_trace
+    net._y_trace = None
+    assert all(t.dtype == torch.float32 for t in traces[True])
+    # (channels-last states padded to the vector width: fp32 12, bf16 16 channels; 10 are real)
+    errs = [((b[..., :10] - a[..., :10]).norm() / a[..., :10].norm().clamp_min(1e-30)).item()
+            for a, b in zip(traces[False], traces[True])]
+    print('RDCNet bf16 vs fp32, residual state y_t relative L2 per step:', ' '.join('%.2e' % e for e in errs))
+    assert max(errs) <= 2e-2, errs
+    assert errs[-1] <= 3.0 * errs[0] + 1e-3, errs
