@@ -31,8 +31,31 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <vector>
+
+#ifndef HCU_CONV8_EXP
+#define HCU_CONV8_EXP 0   // measurement builds only: 1 no MFMA, 2 no output stores, 3 no halo loads,
+                          // 4 second-half blocks start ~3 us late, 5 no next-tile fetch, 6 no LDS reads in the MFMA loop
+#endif
 
 namespace hcu {
+
+#if HCU_CONV8_EXP == 7
+// per-phase cycle totals of wave 0 of every block (measurement builds only):
+// [0] halo -> LDS incl. the prefetch wait, [1] barrier, [2] next-halo issue,
+// [3] MFMA loop, [4] epilogue, [5] tiles, [6] prologue, [7] lifetime
+__device__ unsigned long long g_conv8_phase[8192 * 8];
+#define C8_MARK(k)                                                 \
+  do {                                                             \
+    const long long t__ = (long long)__builtin_readcyclecounter(); \
+    ph[k] += t__ - ph_t;                                           \
+    ph_t = t__;                                                    \
+  } while (0)
+#else
+#define C8_MARK(k) \
+  do {             \
+  } while (0)
+#endif
 
 bool conv8_disabled() {   // HCU_NO_CONV8=1 keeps the 16x16x4 kernels (A/B testing)
   static const bool off = [] {
@@ -62,6 +85,11 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   GConvArgs &sa = *reinterpret_cast<GConvArgs *>(sa_raw);
 #define KA(f) kuni(sa.f)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if HCU_CONV8_EXP == 7
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long long ph_start = (long long)__builtin_readcyclecounter();
+  long long ph_t = ph_start;
+#endif
   if (tid == 0) sa = a;
   const int T = a.KX * a.KY * a.KZ;
   const int HZ = a.HZ, HYZ = a.HY * a.HZ, HV = a.HX * HYZ, HVP = a.HVP;
@@ -72,6 +100,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   int *rowoff = toffs + T;                                       // [128*G] store offsets, -1 past MT
   int *rowpk = rowoff + 128 * G;                                  // [128*G] packed (lx,ly,lz)
   float *pivl = reinterpret_cast<float *>(rowpk + 128 * G);       // [8] statistics pivot
+  float *epil = pivl + 8;   // [5][8] bias, BatchNorm scale, shift, mean, invstd (epilogue)
   const int ntiles = a.ntx * a.nty * a.ntz;
   const int total = a.B * ntiles;
 
@@ -85,10 +114,6 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
   } else {
     for (int i = tid; i < T * C4 * 8; i += 256)
       reinterpret_cast<float4 *>(wlds)[i] = reinterpret_cast<const float4 *>(a.w)[i];
-  }
-  for (int t = tid; t < T; t += 256) {
-    const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
-    toffs[t] = (kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz) * 4;
   }
   for (int m = tid; m < 128 * G; m += 256) {
     int q, lz, lx, ly;
@@ -112,27 +137,41 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     }
     vb[g] = v * 4;
   }
+  // weight column (B operand) of this lane, and the output channels its
+  // accumulators hold: with the weights as the MFMA's first operand, result
+  // register r of lane l is channel 4*(l >> 5) + r of voxel l & 31 of the
+  // group, so a lane stores its voxel's 4 channels as one 16-byte vector
   const int col = ((lane >> 5) << 2) | (lane & 3);
   const int wcol = col * 4;
-  const bool cstore = col < a.OCs, cstat = col < a.Cout;
-  const float bnsc = (BNB && cstat) ? a.bn_scale[col] : 0.f;
-  const float bnsh = (BNB && cstat) ? a.bn_shift[col] : 0.f;
-  const float bnmu = (BNB && cstat) ? a.bn_mean[col] : 0.f;
-  const float bnis = (BNB && cstat) ? a.bn_invstd[col] : 0.f;
-  const float bias = (a.bias && cstat) ? a.bias[col] : 0.f;
+  const int h = lane >> 5;   // channels 4h .. 4h+3
+  const bool hstore = 4 * h < a.OCs;
+  const int ncs = a.Cout - 4 * h;   // channel 4h + r is real when r < ncs
+  if (tid < 40) {
+    const int k = tid >> 3, c = tid & 7;
+    const bool real = c < a.Cout;
+    const float *src = k == 0 ? a.bias : k == 1 ? a.bn_scale : k == 2 ? a.bn_shift : k == 3 ? a.bn_mean : a.bn_invstd;
+    epil[tid] = (real && src && (k == 0 || BNB)) ? src[c] : 0.f;
+  }
   // forward statistics about a block-wide pivot per channel (the value of the
   // block's first output voxel; StatRow in common.h)
   const bool fwdstat = a.stats && !BNB;
-  float s1 = 0.f, s2 = 0.f, cnt = 0.f, piv = 0.f;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  float cnt = 0.f;
   bool have_piv = false;
   const bool act = a.in_scale != nullptr;
   const int S = T * C4;
 
-  // Tap offsets come from the LDS table (toffs, float offsets per tap).
+  // Tap offsets (floats): lane t holds tap t's (T <= 64), read with
+  // v_readlane -- no LDS round trip ahead of each K-step's fragment reads.
+  int toff_lane = 0;
+  if (lane < T) {
+    const int kz = lane % a.KZ, q = lane / a.KZ, ky = q % a.KY, kx = q / a.KY;
+    toff_lane = (kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz) * 4;
+  }
   auto load = [&](int s, floatx4 &bw, floatx4 (&av)[G]) {
     const int t = s / C4, q = s - t * C4;
     bw = *reinterpret_cast<const floatx4 *>(wlds + s * 32 + wcol);
-    const float *ap = alds + (size_t)q * HVP * 4 + toffs[t];
+    const float *ap = alds + (size_t)q * HVP * 4 + __builtin_amdgcn_readlane(toff_lane, t);
 #pragma unroll
     for (int g = 0; g < G; ++g) av[g] = *reinterpret_cast<const floatx4 *>(ap + vb[g]);
   };
@@ -159,6 +198,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
                         : make_float4(1.f, 1.f, 1.f, 1.f);
   const float4 sh = act ? *reinterpret_cast<const float4 *>(a.in_shift + cq)
                         : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float relu_lo = act ? 0.f : -INFINITY;
   // Halo loads go through a buffer descriptor of the tile's batch sample: an
   // element outside the input gets an out-of-range offset, which the hardware
   // range check turns into 0 (no branch per element); BatchNorm+ReLU is
@@ -182,7 +222,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
     oz0 = tzi * KA(TZ);
   };
   // branch-free: invalid elements read an offset past the buffer (-> 0)
-  auto fetch = [&](int tile) {
+  auto fetch = [&](int tile, bool valid) {
     int b, ox0, oy0, oz0;
     tile_origin(tile, b, ox0, oy0, oz0);
     if constexpr (INX > 0) {
@@ -197,7 +237,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       for (int u = 0; u < NPF; ++u) {
         const int hp = hpk[u];
         const int gx = gx0 + (hp >> 20), gy = gy0 + ((hp >> 10) & 1023), gz = gz0 + (hp & 1023);
-        const bool ok = (hp >= 0) & ((hp & 1023) < HZr) & ((unsigned)gx < (unsigned)IX) &
+        const bool ok = valid & (hp >= 0) & ((hp & 1023) < HZr) & ((unsigned)gx < (unsigned)IX) &
                         ((unsigned)gy < (unsigned)IY) & ((unsigned)gz < (unsigned)IZ);
         const int vo = (gx * IY + gy) * IZ + gz;
 #pragma unroll
@@ -225,34 +265,22 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
       const int hp = hpk[u];
       const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
       const int gx = gx0 + hx, gy = gy0 + hy, gz = gz0 + hz;
-      const bool ok = (hp >= 0) & (hz < HZr) & ((unsigned)gx < (unsigned)IX) &
+      const bool ok = valid & (hp >= 0) & (hz < HZr) & ((unsigned)gx < (unsigned)IX) &
                       ((unsigned)gy < (unsigned)IY) & ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
-      pf[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      if (HCU_CONV8_EXP == 3)
+        pf[u] = floatx4{(float)off, 0.f, 0.f, 0.f};
+      else
+        pf[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
   };
-  // The epilogue issues 4*G stores after the next tile's halo loads; where the
-  // path into the halo wait has no epilogue (the first tile) as many stores go
-  // to an empty buffer (dropped), so the compiler's wait for each prefetched
-  // element never includes output stores.
-  auto dummy_epilogue = [&]() {
-    const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, 0, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < 4 * G; ++k) __builtin_amdgcn_raw_buffer_store_b32(0u, zr, 64 * k, 0, 0);
-  };
-  lds_barrier();   // sa and the tables are in LDS
-  // contiguous tile range per block (consecutive tiles share halo rows in L2)
-  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
-  if (t_beg < t_end) fetch(t_beg);
-  dummy_epilogue();
-
-  for (int tile = t_beg; tile < t_end; ++tile) {
+  // The halo image of a tile from the prefetched registers (a tile index past
+  // the block's range was fetched with every element invalid: zeros)
+  auto stage = [&](float *dst, int tile) {
     int b, ox0, oy0, oz0;
     tile_origin(tile, b, ox0, oy0, oz0);
-    lds_barrier();
     // (NCXYZ input) the input voxels this tile owns in the channels-last copy:
     // its output tile's x / y / z range, plus the kernel's overhang on the
     // grid's last tile of each axis
@@ -274,124 +302,180 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
           *reinterpret_cast<floatx4 *>(xclp + vox * 4) = v;
         }
       }
-      if (act) {
-        v[0] = fmaxf(fmaf(v[0], sc.x, sh.x), 0.f);
-        v[1] = fmaxf(fmaf(v[1], sc.y, sh.y), 0.f);
-        v[2] = fmaxf(fmaf(v[2], sc.z, sh.z), 0.f);
-        v[3] = fmaxf(fmaf(v[3], sc.w, sh.w), 0.f);
-      }
+      // BatchNorm+ReLU, branch-free (no input BatchNorm: scale 1, shift 0,
+      // floor -inf)
+      v[0] = fmaxf(fmaf(v[0], sc.x, sh.x), relu_lo);
+      v[1] = fmaxf(fmaf(v[1], sc.y, sh.y), relu_lo);
+      v[2] = fmaxf(fmaf(v[2], sc.z, sh.z), relu_lo);
+      v[3] = fmaxf(fmaf(v[3], sc.w, sh.w), relu_lo);
       const bool ok = (okbits >> u) & 1u;
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       // elements past the halo write the unused last slot of the last plane
       const int slot = hpk[u] >= 0 ? (idx % C4) * HVP + idx / C4 : C4 * HVP - 1;
-      *reinterpret_cast<floatx4 *>(alds + (size_t)slot * 4) = ok ? v : z;
+      *reinterpret_cast<floatx4 *>(dst + (size_t)slot * 4) = ok ? v : z;
     }
+  };
+  lds_barrier();   // sa and the tables are in LDS
+  // contiguous tile range per block (consecutive tiles share halo rows in L2)
+  const int tpb_ = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_beg = blockIdx.x * tpb_, t_end = min(total, t_beg + tpb_);
+  if (t_beg < t_end) fetch(t_beg, true);
+  // The epilogue issues G stores after the next tile's halo loads; where the
+  // path into the halo wait has no epilogue (the first tile) as many stores go
+  // to an empty buffer (dropped), so the compiler's wait for each prefetched
+  // element never includes output stores.
+  {
+    const __amdgpu_buffer_rsrc_t zr = __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, 0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < G; ++k) __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, zr, 256 * k, 0, 0);
+  }
+  C8_MARK(6);
+
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    int b, ox0, oy0, oz0;
+    tile_origin(tile, b, ox0, oy0, oz0);
+    // output row offsets of this tile
+    const int OX = KA(OX), OY = KA(OY), OZ = KA(OZ), OCs = KA(OCs), SY = KA(SY), SZ = KA(SZ);
+    const int sample = KA(SX) * SY * SZ * OCs;
+    const int tbase = (((ox0 * SY + oy0) * SZ + oz0) * OCs + 4 * h) * 4;
+    const bool interior = ox0 + KA(TX) <= OX && oy0 + KA(TY) <= OY && oz0 + KA(TZ) <= OZ;
+    int ro[G];
+    const int mb = wave * G * 32 + (lane & 31);
+#pragma unroll
+    for (int g = 0; g < G; ++g) ro[g] = rowoff[mb + g * 32];
+    if (!interior) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int pk = rowpk[mb + g * 32];
+        const bool in = (ox0 + (pk >> 20) < OX) & (oy0 + ((pk >> 10) & 1023) < OY) & (oz0 + (pk & 1023) < OZ);
+        ro[g] = in ? ro[g] : -1;
+      }
+    }
+    C8_MARK(0);
+    lds_barrier();   // the previous tile's MFMAs are done with the halo image
+    stage(alds, tile);
     lds_barrier();
-    if (tile + 1 < t_end) fetch(tile + 1);
+    if (HCU_CONV8_EXP != 5 && tile + 1 < t_end) fetch(tile + 1, true);
+    C8_MARK(1);
     // ---- MFMA over the K-steps, next step's fragments loaded ahead
     floatx4 acc[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+    auto mf = [&](int c, float w, float x, int g) {
+      acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(w, x, acc[g], 0, 0, 0);
+    };
     floatx4 b0, b1, a0[G], a1[G];
     load(0, b0, a0);
-    for (int s = 0; s < S; s += 2) {
+    for (int s = 0; s < (HCU_CONV8_EXP == 1 ? 0 : S); s += 2) {
+      if (HCU_CONV8_EXP == 6) {
+        b1 = b0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) a1[g] = a0[g];
+      } else
       load(min(s + 1, S - 1), b1, a1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
         for (int g = 0; g < G; ++g)
-          acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(a0[g][c], b0[c], acc[g], 0, 0, 0);
-      load(min(s + 2, S - 1), b0, a0);
+          mf(c, b0[c], a0[g][c], g);
+      if (HCU_CONV8_EXP != 6) load(min(s + 2, S - 1), b0, a0);
       __builtin_amdgcn_sched_barrier(0);
       if (s + 1 < S) {
 #pragma unroll
         for (int c = 0; c < 4; ++c)
 #pragma unroll
           for (int g = 0; g < G; ++g)
-            acc[g] = __builtin_amdgcn_mfma_f32_4x4x1f32(a1[g][c], b1[c], acc[g], 0, 0, 0);
+            mf(c, b1[c], a1[g][c], g);
       }
     }
-    // ---- epilogue: bias, store, BatchNorm partial statistics.  The store
-    // offsets are read from LDS up front (one wait), and the output pointer is
-    // a global-address-space pointer so the stores cannot alias LDS and do not
-    // serialise the table reads.
-    const int OX = KA(OX), OY = KA(OY), OZ = KA(OZ), OCs = KA(OCs), SY = KA(SY), SZ = KA(SZ);
-    const int sample = KA(SX) * SY * SZ * OCs;
-    // per-sample buffers (32-bit offsets within one sample)
+    C8_MARK(3);
+    // ---- epilogue: bias, store (per-sample buffer, 32-bit offsets), BatchNorm
+    // partial statistics
     const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
         (void *)(KA(out) + (size_t)b * sample), 0, sample * 4, 0x00020000);
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        BNB ? (void *)(KA(bn_y) + (size_t)b * sample) : (void *)a.in, 0, BNB ? sample * 4 : 0,
-        0x00020000);
-    const int tbase = (((ox0 * SY + oy0) * SZ + oz0) * OCs + col) * 4;
-    const bool interior = ox0 + KA(TX) <= OX && oy0 + KA(TY) <= OY && oz0 + KA(TZ) <= OZ;
-    int ro[G * 4];
-    const int mb = wave * G * 32 + ((lane >> 2) & 7) * 4;
+    const floatx4 bias = *reinterpret_cast<const floatx4 *>(epil + 4 * h);
+    if (fwdstat && !have_piv) {   // block-uniform: the first tile of this block
+      if (wave == 0 && (lane & 31) == 0)
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) ro[g * 4 + rr] = rowoff[mb + g * 32 + rr];
-    if (!interior) {
+        for (int r = 0; r < 4; ++r) pivl[4 * h + r] = acc[0][r] + bias[r];
+      lds_barrier();
+      have_piv = true;
+    }
+    const floatx4 piv = fwdstat ? *reinterpret_cast<const floatx4 *>(pivl + 4 * h) : floatx4{0.f, 0.f, 0.f, 0.f};
+    // fused BatchNorm+ReLU backward: the layer's output y of the same voxels
+    // (loaded after the MFMAs: the next halo's loads, issued before them, have
+    // landed by then, so waiting for y costs nothing extra)
+    floatx4 yv[G];
+    floatx4 bnsc, bnsh, bnmu, bnis;
+    if constexpr (BNB) {
+      const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(KA(bn_y) + (size_t)b * sample), 0, sample * 4, 0x00020000);
 #pragma unroll
       for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int pk = rowpk[mb + g * 32 + rr];
-          const bool in = (ox0 + (pk >> 20) < OX) & (oy0 + ((pk >> 10) & 1023) < OY) &
-                          (oz0 + (pk & 1023) < OZ);
-          ro[g * 4 + rr] = in ? ro[g * 4 + rr] : -1;
-        }
-    }
-    if (fwdstat && !have_piv) {   // block-uniform: the first tile of this block
-      if (wave == 0 && ((lane >> 2) & 7) == 0) pivl[col] = acc[0][0] + bias;
-      lds_barrier();
-      piv = pivl[col];
-      have_piv = true;
+        yv[g] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                yrs, ro[g] >= 0 ? tbase + ro[g] * 4 : 0x7ffffff0, 0, 0));
+      bnsc = *reinterpret_cast<const floatx4 *>(epil + 8 + 4 * h);
+      bnsh = *reinterpret_cast<const floatx4 *>(epil + 16 + 4 * h);
+      bnmu = *reinterpret_cast<const floatx4 *>(epil + 24 + 4 * h);
+      bnis = *reinterpret_cast<const floatx4 *>(epil + 32 + 4 * h);
     }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
+      const int o = ro[g];
+      floatx4 v;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int o = ro[g * 4 + rr];
-        float v = acc[g][rr] + bias;
-        float w2 = v - piv, w1 = v - piv;
-        if (BNB) {   // fused BatchNorm+ReLU backward: v = dA -> dz, stats (dz, dz*xhat)
-          const float yv = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(yrs, o >= 0 ? tbase + o * 4 : 0x7ffffff0, 0, 0));
-          v = fmaf(yv, bnsc, bnsh) > 0.f ? v : 0.f;
-          w1 = v;
-          w2 = (yv - bnmu) * bnis;
+      for (int r = 0; r < 4; ++r) {
+        float x = acc[g][r] + bias[r];
+        float w1 = x - piv[r], w2 = x - piv[r];
+        if (BNB) {   // v = dA -> dz, stats (dz, dz*xhat)
+          x = fmaf(yv[g][r], bnsc[r], bnsh[r]) > 0.f ? x : 0.f;
+          w1 = x;
+          w2 = (yv[g][r] - bnmu[r]) * bnis[r];
         }
-        __builtin_amdgcn_raw_buffer_store_b32(
-            __builtin_bit_cast(uint32_t, v), ors,
-            (o >= 0 && cstore) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
-        const bool ok = o >= 0 && cstat;
-        const float w = ok ? w1 : 0.f;
-        s1 += w;
-        s2 = fmaf(w, w2, s2);
-        cnt += ok ? 1.f : 0.f;
+        v[r] = x;
+        const float w = (o >= 0 && r < ncs) ? w1 : 0.f;
+        s1[r] += w;
+        s2[r] = fmaf(w, w2, s2[r]);
       }
+      cnt += o >= 0 ? 1.f : 0.f;
+      if (HCU_CONV8_EXP != 2 || v[0] == 1234.5f)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ors,
+                                               (o >= 0 && hstore) ? tbase + o * 4 : 0x7ffffff0, 0, 0);
     }
+    C8_MARK(4);
+#if HCU_CONV8_EXP == 7
+    ph[5] += 1;
+#endif
   }
+#if HCU_CONV8_EXP == 7
+  if (tid == 0) {
+    unsigned long long *d = g_conv8_phase + (size_t)(blockIdx.x % 8192) * 8;
+    for (int k = 0; k < 7; ++k) d[k] += (unsigned long long)ph[k];
+    d[7] += (unsigned long long)((long long)__builtin_readcyclecounter() - ph_start);
+  }
+#endif
   if (!a.stats) return;
-  // lanes sharing a channel differ in lane bits 2..4: fixed-order butterfly
-  s1 += __shfl_xor(s1, 4);
-  s2 += __shfl_xor(s2, 4);
-  cnt += __shfl_xor(cnt, 4);
-  s1 += __shfl_xor(s1, 8);
-  s2 += __shfl_xor(s2, 8);
-  cnt += __shfl_xor(cnt, 8);
-  s1 += __shfl_xor(s1, 16);
-  s2 += __shfl_xor(s2, 16);
-  cnt += __shfl_xor(cnt, 16);
+  // lanes sharing channels (the 32 voxels of a half): fixed-order butterfly
+#pragma unroll
+  for (int m = 1; m < 32; m <<= 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] += __shfl_xor(s1[r], m);
+      s2[r] += __shfl_xor(s2[r], m);
+    }
+    cnt += __shfl_xor(cnt, m);
+  }
   lds_barrier();
   float *red = smem;  // [4 waves][8 channels][3]
-  if (((lane >> 2) & 7) == 0) {
-    red[(wave * 8 + col) * 3 + 0] = s1;
-    red[(wave * 8 + col) * 3 + 1] = s2;
-    red[(wave * 8 + col) * 3 + 2] = cnt;
-  }
+  if ((lane & 31) == 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = 4 * h + r;
+      red[(wave * 8 + c) * 3 + 0] = s1[r];
+      red[(wave * 8 + c) * 3 + 1] = s2[r];
+      red[(wave * 8 + c) * 3 + 2] = r < ncs ? cnt : 0.f;
+    }
   lds_barrier();
   if (tid < 8) {
     float t1 = 0.f, t2 = 0.f, tn = 0.f;
@@ -415,7 +499,7 @@ __global__ void __launch_bounds__(256, 2) conv8_kernel(const GConvArgs a) {
 // ---------------------------------------------------------------------------
 static long conv8_lds(const GConvArgs &a, int C4, int HVP, int G) {
   const int T = a.KX * a.KY * a.KZ;
-  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G + 8) * 4 +
+  return ((long)C4 * HVP * 4 + (long)T * C4 * 32 + T + 2L * 128 * G + 8 + 40) * 4 +
          (long)sizeof(GConvArgs);   // + the static copy of the arguments
 }
 
@@ -426,7 +510,7 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   if (conv8_disabled()) return 1;
   if (a.nph > 1 || a.sx != 1 || a.sy != 1 || a.sz != 1) return 1;
   if (a.osx != 1 || a.osy != 1 || a.osz != 1 || a.ofx || a.ofy || a.ofz) return 1;
-  if (a.Cout > 8 || a.OCs > 8 || a.ICs % 4) return 1;
+  if (a.Cout > 8 || a.OCs > 8 || a.ICs % 4 || a.KX * a.KY * a.KZ > 64) return 1;
   const int C4 = a.ICs / 4;
   if (C4 != 1 && C4 != 2 && C4 != 4) return 1;
   if (a.OX <= 0 || a.OY <= 0 || a.OZ <= 0) return 2;
@@ -452,8 +536,8 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
     const int HVP = round_up(HV, 16) + 8;
     const long lds = conv8_lds(a, C4, HVP, G);
     const long tiles = (long)a.B * cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz;
-    // <= 12 prefetched elements per thread (16 spills registers at G = 8; 16
-    // at G <= 4, which lets d1.c1's input gradient take G = 4, measured equal)
+    // two workgroups per CU; <= 12 prefetched elements per thread (16 spills
+    // registers at G = 8)
     if (lds > 80 * 1024 || HV * C4 > 12 * 256) continue;
     a.G8 = G;
     a.TX = TX;
@@ -491,8 +575,7 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   a.fKZ = FastDiv(a.KZ);
   a.fKY = FastDiv(a.KY);
   const long tiles = (long)a.B * a.ntx * a.nty * a.ntz;
-  const int occ = std::max(1, std::min(4, (int)(160 * 1024 / a.lds_bytes)));
-  a.gridx = (int)std::min<long>(tiles, 256L * occ);
+  a.gridx = (int)std::min<long>(tiles, 512L);   // two persistent workgroups per CU
   a.use_conv8 = 1;
   a.use_conv2 = 0;
   return 0;
@@ -524,6 +607,19 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
   }
 #define CONV8_NPF(C4_, G_) \
   CONV8_CASE(C4_, G_, 8) else CONV8_CASE(C4_, G_, 12) else CONV8_CASE(C4_, G_, 16)
+
+#if HCU_CONV8_EXP == 7
+// the phase totals (measurement builds): sums over the blocks, then zeroed
+extern "C" int hcu_debug_conv8_phases(unsigned long long *out) {
+  std::vector<unsigned long long> h(8192 * 8);
+  if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_conv8_phase), h.size() * 8) != hipSuccess) return 3;
+  for (int k = 0; k < 8; ++k) out[k] = 0;
+  for (size_t i = 0; i < h.size(); ++i) out[i % 8] += h[i];
+  std::fill(h.begin(), h.end(), 0ull);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_conv8_phase), h.data(), h.size() * 8) != hipSuccess) return 3;
+  return 0;
+}
+#endif
 
 int launch_conv8(const GConvArgs &a, hipStream_t s) {
   const int C4 = a.ICs / 4;

@@ -134,7 +134,7 @@ def check_grads(m, spec, p32, p64, rl2_max=RL2_MAX):
     return worst
 
 
-def check_adam(m, spec, p64, frac=2e-3):
+def check_adam(m, spec, p64, p32, frac=2e-3, lr=1e-3):
     params = dict(m.named_parameters())
     for n in uo.param_names(spec):
         if _bn_cancelled(n):
@@ -142,7 +142,15 @@ def check_adam(m, spec, p64, frac=2e-3):
         a = params[n].detach().cpu().double()
         b = p64['state_after'][n].double()
         # one Adam step moves each weight by ~lr (p - lr*g/(|g|+eps) at step 1)
-        bad = ((a - b).abs() > 1e-5).double().mean().item()
+        assert (a - b).abs().max().item() <= 2.0 * lr + 1e-6, n
+        diff = (a - b).abs() > 1e-5
+        # where |g| is within the fp32 reference's own gradient error, the sign
+        # of that step is not determined by fp32 arithmetic (the reference's
+        # fp32 step differs from fp64 there too): only determined entries count
+        g64 = p64['grads'][n].double()
+        noise = (p32['grads'][n].double() - g64).abs().max().item()
+        diff &= g64.abs() > 8.0 * noise
+        bad = diff.double().mean().item()
         assert bad <= frac, (n, bad)
 
 
@@ -171,7 +179,7 @@ def test_train_step_parity(name):
     check_running_stats(m, spec, ref32)
     opt.step()
     torch.cuda.synchronize()
-    check_adam(m, spec, p64)
+    check_adam(m, spec, p64, p32)
     # eval-mode forward with the updated weights and running stats
     m.eval()
     with torch.no_grad():
@@ -238,7 +246,7 @@ def test_full_config2_train_step():
     check_running_stats(m, spec, ref32)
     opt.step()
     torch.cuda.synchronize()
-    check_adam(m, spec, p64)
+    check_adam(m, spec, p64, p32)
 
 
 def test_deterministic_bitwise():
