@@ -130,6 +130,9 @@ SYMBOLS = [
                                   ctypes.POINTER(_SZ)]),
     ("hcu_chain_forward", _I, [_VP, ctypes.POINTER(UnetTensors), _I, _VP]),
     ("hcu_chain_backward", _I, [_VP, ctypes.POINTER(UnetTensors), _VP, _VP, _I, _I, _VP]),
+    ("hcu_chain_weight_image_bytes", _SZ, [_VP]),
+    ("hcu_chain_forward_images", _I, [_VP, ctypes.POINTER(UnetTensors), _I, _VP, _VP, _I]),
+    ("hcu_chain_backward_images", _I, [_VP, ctypes.POINTER(UnetTensors), _VP, _VP, _I, _I, _VP, _VP, _I]),
     ("hcu_gate_fwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_gate_bwd", _I, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_gather_vectors", _I, [ctypes.POINTER(_VP), ctypes.POINTER(_I), _I, _VP, _I, _VP]),

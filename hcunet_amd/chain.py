@@ -287,6 +287,23 @@ class Chain:
         return _ChainFunction.apply(x, self, bool(training), bool(bf16), *params)
 
 
+# Bumped by hcunet_amd.optim.Adam (which writes the parameters through raw
+# pointers, bypassing their version counters) and invalidate_weight_images().
+_WEIGHT_EPOCH = [0]
+
+
+def invalidate_weight_images():
+    """Forces every chain to re-lay its packed weight images on its next call:
+    needed after parameter writes that bypass the tensors' version counters
+    (through .data or raw pointers); in-place torch ops, load_state_dict and
+    hcunet_amd.optim.Adam are tracked already."""
+    _WEIGHT_EPOCH[0] += 1
+
+
+def _weight_key(chain):
+    return (chain.flat.flat.data_ptr(), _WEIGHT_EPOCH[0]) + tuple(p._version for p in chain.flat.params)
+
+
 class _ChainPlan:
     def __init__(self, spec, B, X, Y, Z):
         L = _lib.lib()
@@ -301,6 +318,21 @@ class _ChainPlan:
         self.n_bn = int(nbn.value)
         self.saved_bytes = int(sv.value)
         self.scratch_bytes = int(sc.value)
+        # packed weight images kept across calls (the last image_bytes of
+        # `saved` otherwise): re-laid only when the parameters changed
+        self.image_bytes = int(L.hcu_chain_weight_image_bytes(h))
+        self.images = None
+        self.image_key = None
+        self.image_level = 0   # 1: forward images of image_key, 2: also the input-gradient ones
+
+    def images_for(self, key, dev):
+        """The image buffer and how much of it holds the images of `key`."""
+        if self.images is None or self.images.device != dev:
+            self.images = torch.empty(max(self.image_bytes, 16), dtype=torch.uint8, device=dev)
+            self.image_key, self.image_level = None, 0
+        if key != self.image_key:
+            self.image_key, self.image_level = key, 0
+        return self.images, self.image_level
 
     def __del__(self):
         try:
@@ -341,15 +373,20 @@ class _ChainFunction(torch.autograd.Function):
                               device=dev)
         else:
             out = torch.empty(plan.out_shape, dtype=torch.float32, device=dev)
-        saved = torch.empty(max(plan.saved_bytes, 1), dtype=torch.uint8, device=dev)
+        # the weight images live in the plan's persistent buffer (the end of
+        # `saved` is not needed)
+        saved = torch.empty(max(plan.saved_bytes - plan.image_bytes, 1), dtype=torch.uint8, device=dev)
         scratch = torch.empty(max(plan.scratch_bytes, 1), dtype=torch.uint8, device=dev)
         t = _tensors(chain, x, out, saved, scratch)
         L = _lib.lib()
         if TAG_CHAINS:
             L.hcu_timing_prefix(chain.name.encode())
+        images, level = plan.images_for(_weight_key(chain), dev)
         with torch.cuda.device(dev):
-            _lib.check(L.hcu_chain_forward(plan.handle, ctypes.byref(t), 1 if training else 0,
-                                           _lib.stream_handle(dev)), 'chain forward')
+            _lib.check(L.hcu_chain_forward_images(plan.handle, ctypes.byref(t), 1 if training else 0,
+                                                  _lib.stream_handle(dev), ctypes.c_void_p(images.data_ptr()),
+                                                  level), 'chain forward')
+        plan.image_level = 2 if training else max(level, 1)
         if TAG_CHAINS:
             L.hcu_timing_prefix(b'')
         ctx.chain, ctx.plan, ctx.training, ctx.bf16 = chain, plan, training, bf16
@@ -376,10 +413,12 @@ class _ChainFunction(torch.autograd.Function):
         if TAG_CHAINS:
             L.hcu_timing_prefix(chain.name.encode())
         with torch.cuda.device(dev):
-            _lib.check(L.hcu_chain_backward(plan.handle, ctypes.byref(t),
-                                            ctypes.c_void_p(dout.data_ptr()), _lib.ptr(dx),
-                                            1 if ctx.training else 0, 1, _lib.stream_handle(dev)),
+            _lib.check(L.hcu_chain_backward_images(plan.handle, ctypes.byref(t),
+                                                   ctypes.c_void_p(dout.data_ptr()), _lib.ptr(dx),
+                                                   1 if ctx.training else 0, 1, _lib.stream_handle(dev),
+                                                   ctypes.c_void_p(plan.images.data_ptr()), plan.image_level),
                        'chain backward')
+        plan.image_level = 2
         if TAG_CHAINS:
             L.hcu_timing_prefix(b'')
         finish()

@@ -529,6 +529,8 @@ struct hcu_unet_plan {
   // per decoder level: the column-sum rows of dU (the up_conv bias gradient)
   // written by the folded conv1's input-gradient kernel
   size_t colsum_off[HCU_MAX_LEVELS] = {};
+  // layer chains: the packed weight images are saved[img_lo, img_lo + img_bytes)
+  size_t img_lo = 0, img_bytes = 0;
   double fwd_flops = 0.0;   // forward convolution FLOPs (graph replay only below 100 GFLOP)
   // Layer-chain plans (hcu_chain_*): a sequence of ops instead of the U-Net.
   struct ChainOp {
@@ -894,6 +896,11 @@ struct Ctx {
   int next_slot = 0;
   unsigned slot_read = 0;   // slots whose last reader event was recorded in this enqueue
   float *fptr(char *base, size_t off) const { return reinterpret_cast<float *>(base + off); }
+  // Base of the packed weight images (offsets wf_off / wd_off / wph_off): the
+  // saved workspace, or a layer chain's caller-owned image buffer
+  // (hcu_chain_forward_images), which then starts at plan offset img_lo.
+  char *wi = nullptr;
+  char *wimg() const { return wi ? wi : sv; }
   int bf() const { return p.es == 2; }   // bf16 activation storage
   float *part() const { return fptr(sc, p.part_off); }
   float *wpart() const { return fptr(sc, split ? p.wpart_off : p.part_off); }
@@ -1010,7 +1017,7 @@ int conv_forward(const Ctx &c, const ConvLayer &L, const float *in, const float 
   if (in_fmt) a.w = c.P + L.w_off;   // (read in the PyTorch layout by the NCXYZ staging)
   a.in_scale = isc;
   a.in_shift = ish;
-  if (!in_fmt) a.w = c.fptr(c.sv, L.wf_off);
+  if (!in_fmt) a.w = c.fptr(c.wimg(), L.wf_off);
   a.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
   a.out = c.fptr(c.sv, L.y_off);
   a.stats = training ? c.part() : nullptr;
@@ -1098,7 +1105,7 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   tag(L.name, "dgrad");
   GConvArgs a = L.dgrad;
   a.in = dy;
-  a.w = c.fptr(c.sv, L.wd_off);
+  a.w = c.fptr(c.wimg(), L.wd_off);
   a.out = dA;
   a.partial = c.kpart();
   const bool fused = fuse_bnbwd(c, a, bnl);
@@ -1376,26 +1383,26 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   if (split && training) {
     if (int e = c.fork()) return e;
     if (p.prep_fwd.size() > n0) {
-      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data() + n0,
+      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_fwd.data() + n0,
                                   (int)(p.prep_fwd.size() - n0), c.ws))
         return e;
       ev_rest = p.ev_fork_ring[p.fork_next++ % HCU_FORK_RING];
       HCU_HIP(hipEventRecord(ev_rest, c.ws));
     }
     if (!p.prep_bwd.empty())
-      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
+      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_bwd.data(),
                                   (int)p.prep_bwd.size(), c.ws))
         return e;
-    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data(), (int)n0, c.s))
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_fwd.data(), (int)n0, c.s))
       return e;
   } else {
     if (training && !p.prep_bwd.empty()) {
       if (int e = c.fork()) return e;
-      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(),
+      if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_bwd.data(),
                                   (int)p.prep_bwd.size(), c.wstream()))
         return e;
     }
-    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_fwd.data(),
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_fwd.data(),
                                 (int)p.prep_fwd.size(), c.s))
       return e;
   }
@@ -1433,7 +1440,7 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
       a.in = src;
       a.in_scale = ssc;
       a.in_shift = ssh;
-      a.w = c.fptr(c.sv, u.wf_off);
+      a.w = c.fptr(c.wimg(), u.wf_off);
       a.bias = c.P + u.b_off;
       a.out = U;
       a.stats = nullptr;
@@ -1445,7 +1452,7 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
       a.in = src;
       a.in_scale = ssc;
       a.in_shift = ssh;
-      a.w = c.fptr(c.sv, u.wph_off[ph]);
+      a.w = c.fptr(c.wimg(), u.wph_off[ph]);
       a.bias = c.P + u.b_off;
       a.out = U;
       a.stats = nullptr;
@@ -1529,7 +1536,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
   // an eval-mode forward prepared only the forward weight images: the
   // input-gradient images are laid out here
   if (!training && !p.prep_bwd.empty())
-    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(),
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_bwd.data(), (int)p.prep_bwd.size(),
                                 c.s))
       return e;
   int cur = 0;  // slot holding the current d(pre-BN y) (or dz, Ctx::ap)
@@ -1654,7 +1661,7 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
       float *dP = c.buf(sd);
       GConvArgs a = u.dgrad;
       a.in = dU;
-      a.w = c.fptr(c.sv, u.wd_off);
+      a.w = c.fptr(c.wimg(), u.wd_off);
       a.out = dP;
       a.partial = c.kpart();
       const bool fused = fuse_bnbwd(c, a, &prev);
@@ -2207,7 +2214,9 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
   }
   p.outd = cur;
   p.n_bn = bn_index;
-  // weight re-layouts (one batched launch per forward)
+  // weight re-layouts (one batched launch per forward), the last range of
+  // `saved` (or the caller's image buffer: hcu_chain_forward_images)
+  const size_t img0 = saved.off;
   p.prep_jobs.clear();
   auto add_job = [&](int kind, size_t n, int64_t src, const WPack &pk, const int *prm, int np, size_t &off) {
     PrepJob j{};
@@ -2258,6 +2267,8 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
   p.prep_bwd.clear();
   for (const PrepJob &j : p.prep_jobs)
     (j.kind == PREP_CONV_DGRAD || j.kind == PREP_CONVT_DGRAD ? p.prep_bwd : p.prep_fwd).push_back(j);
+  p.img_lo = img0;
+  p.img_bytes = saved.off - img0;
   p.saved_bytes = saved.off;
   Region scratch;
   for (int i = 0; i < HCU_NBUF; ++i) p.buf_off[i] = scratch.take_floats(i < p.nbuf ? p.max_act : 0);
@@ -2304,8 +2315,13 @@ std::vector<ChainAct> chain_inputs(const hcu_unet_plan &p, char *sv, const void 
   return in;
 }
 
-int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training, hipStream_t s) {
+// images: the caller's weight-image buffer (img_bytes) or null (in `saved`);
+// images_current: 1 = it holds this plan's forward images of the current
+// parameters, 2 = also the input-gradient ones (no re-layout then).
+int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int training, hipStream_t s,
+                          void *images = nullptr, int images_current = 0) {
   Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  if (images) c.wi = (char *)images - p.img_lo;
   const int es = p.es, bf = c.bf();
   tag(std::string("chain"), "fwd");
   if (!p.in_cl)
@@ -2313,8 +2329,8 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
                              t->x_dtype))
       return e;
   const std::vector<PrepJob> &jobs = training ? p.prep_jobs : p.prep_fwd;
-  if (!jobs.empty())
-    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), jobs.data(), (int)jobs.size(), s)) return e;
+  if (!jobs.empty() && images_current < (training ? 2 : 1))
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), jobs.data(), (int)jobs.size(), s)) return e;
   ChainAct last;
   const std::vector<ChainAct> in = chain_inputs(p, c.sv, t->x, &last);
   for (size_t i = 0; i < p.chain.size(); ++i) {
@@ -2333,7 +2349,7 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
         GConvArgs g = L.fwd;
         g.in = xs;
         g.in_scale = g.in_shift = nullptr;
-        g.w = c.fptr(c.sv, L.wf_off);
+        g.w = c.fptr(c.wimg(), L.wf_off);
         g.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
         g.out = ys;
         g.stats = nullptr;
@@ -2348,7 +2364,7 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
         g.in = a.x;
         g.in_scale = a.sc;
         g.in_shift = a.sh;
-        g.w = c.fptr(c.sv, L.wf_off);
+        g.w = c.fptr(c.wimg(), L.wf_off);
         g.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
         g.out = y;
         g.stats = nullptr;
@@ -2372,7 +2388,7 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
         g.in = a.x;
         g.in_scale = a.sc;
         g.in_shift = a.sh;
-        g.w = c.fptr(c.sv, u.wf_off);
+        g.w = c.fptr(c.wimg(), u.wf_off);
         g.bias = bias;
         g.out = U;
         g.stats = nullptr;
@@ -2384,7 +2400,7 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
         g.in = a.x;
         g.in_scale = a.sc;
         g.in_shift = a.sh;
-        g.w = c.fptr(c.sv, u.wph_off[ph]);
+        g.w = c.fptr(c.wimg(), u.wph_off[ph]);
         g.bias = bias;
         g.out = U;
         g.stats = nullptr;
@@ -2408,14 +2424,16 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
 }
 
 int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout, float *dx,
-                           int training, int accumulate, hipStream_t s) {
+                           int training, int accumulate, hipStream_t s, const void *images = nullptr,
+                           int images_current = 0) {
   Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
+  if (images) c.wi = (char *)images - p.img_lo;
   const int es = p.es, bf = c.bf();
   const int n = (int)p.chain.size();
   const std::vector<ChainAct> in = chain_inputs(p, c.sv, t->x, nullptr);
   // an eval-mode forward prepared only the forward weight images
-  if (!training && !p.prep_bwd.empty())
-    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.sv), p.prep_bwd.data(), (int)p.prep_bwd.size(), s))
+  if (!training && !p.prep_bwd.empty() && images_current < 2)
+    if (int e = launch_prep_all(c.P, reinterpret_cast<float *>(c.wimg()), p.prep_bwd.data(), (int)p.prep_bwd.size(), s))
       return e;
   int cur = 0;
   if (int e = c.alloc(cur)) return e;
@@ -2532,7 +2550,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
       }
       GConvArgs g = u.dgrad;
       g.in = dU;
-      g.w = c.fptr(c.sv, u.wd_off);
+      g.w = c.fptr(c.wimg(), u.wd_off);
       g.out = dP;
       g.partial = c.kpart();
       const ConvLayer *bnl = (pr && pr->kind == HCU_CHAIN_CONV && pr->bn_relu) ? &pr->conv : nullptr;
@@ -2592,8 +2610,16 @@ int hcu_chain_plan_query(const hcu_unet_plan *p, int64_t *out_shape, int *n_bn, 
   return HCU_OK;
 }
 
+static int hcu_chain_forward_impl(const hcu_unet_plan *p, const hcu_unet_tensors *t, int training,
+                                  hcu_stream_t stream, void *images, int images_current);
+
 int hcu_chain_forward(const hcu_unet_plan *p, const hcu_unet_tensors *t, int training, hcu_stream_t stream) {
   if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
+  return hcu_chain_forward_impl(p, t, training, stream, nullptr, 0);
+}
+
+static int hcu_chain_forward_impl(const hcu_unet_plan *p, const hcu_unet_tensors *t, int training,
+                                  hcu_stream_t stream, void *images, int images_current) {
   if (!t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
     return fail(HCU_ERR_INVALID, "null argument");
   if (t->x_dtype != HCU_F32 && t->x_dtype != HCU_F16 && !(t->x_dtype == HCU_BF16 && p->es == 2))
@@ -2606,15 +2632,31 @@ int hcu_chain_forward(const hcu_unet_plan *p, const hcu_unet_tensors *t, int tra
         return fail(HCU_ERR_INVALID, "Expected more than 1 value per channel when training");
   if (p->n_bn && (!t->bn_running_mean || !t->bn_running_var))
     return fail(HCU_ERR_INVALID, "BatchNorm running statistics missing");
-  return enqueue_chain_forward(*p, t, training, (hipStream_t)stream);
+  return enqueue_chain_forward(*p, t, training, (hipStream_t)stream, images, images_current);
 }
 
 int hcu_chain_backward(const hcu_unet_plan *p, const hcu_unet_tensors *t, const float *dout, float *dx,
                        int training, int accumulate, hcu_stream_t stream) {
+  return hcu_chain_backward_images(p, t, dout, dx, training, accumulate, stream, nullptr, 0);
+}
+
+size_t hcu_chain_weight_image_bytes(const hcu_unet_plan *p) { return p && p->is_chain ? p->img_bytes : 0; }
+
+int hcu_chain_forward_images(const hcu_unet_plan *p, const hcu_unet_tensors *t, int training,
+                             hcu_stream_t stream, void *images, int images_current) {
+  if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
+  if (!images) return fail(HCU_ERR_INVALID, "null weight-image buffer");
+  if (images_current < 0 || images_current > 2) return fail(HCU_ERR_INVALID, "images_current must be 0, 1 or 2");
+  return hcu_chain_forward_impl(p, t, training, stream, images, images_current);
+}
+
+int hcu_chain_backward_images(const hcu_unet_plan *p, const hcu_unet_tensors *t, const float *dout, float *dx,
+                              int training, int accumulate, hcu_stream_t stream, const void *images,
+                              int images_current) {
   if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
   if (!t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)
     return fail(HCU_ERR_INVALID, "null argument");
-  return enqueue_chain_backward(*p, t, dout, dx, training, accumulate, (hipStream_t)stream);
+  return enqueue_chain_backward(*p, t, dout, dx, training, accumulate, (hipStream_t)stream, images, images_current);
 }
 
 }  // extern "C"

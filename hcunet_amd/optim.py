@@ -182,4 +182,8 @@ class Adam(torch.optim.Optimizer):
                         _lib.ptr(p), _lib.ptr(g), _lib.ptr(s['exp_avg']), _lib.ptr(s['exp_avg_sq']),
                         p.numel(), group['lr'], b1, b2, group['eps'], group['weight_decay'],
                         int(float(s['step'])), 1.0, stream), 'Adam.step')
+        # the parameters changed behind their version counters: layer chains
+        # re-lay their packed weight images on their next call
+        from . import chain as _chain
+        _chain.invalidate_weight_images()
         return loss

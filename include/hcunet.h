@@ -225,6 +225,21 @@ int hcu_chain_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int 
                       hcu_stream_t stream);
 int hcu_chain_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, const float *dout,
                        float *dx, int training, int accumulate, hcu_stream_t stream);
+/* The same with the packed weight images (the executor's re-layout of the
+ * op weights, normally rebuilt in `saved` by every forward) kept in a
+ * caller-owned buffer of hcu_chain_weight_image_bytes(plan) that outlives the
+ * calls: a recurrence applying one chain several times per step re-lays them
+ * once.  images_current: 0 = re-lay (the parameters changed since the images
+ * were written), 1 = the buffer holds the forward images of the current
+ * parameters (an eval forward wrote it), 2 = forward and input-gradient
+ * images (a training forward wrote it).  The backward must be given the
+ * buffer its forward used. */
+size_t hcu_chain_weight_image_bytes(const hcu_unet_plan *plan);
+int hcu_chain_forward_images(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
+                             hcu_stream_t stream, void *images, int images_current);
+int hcu_chain_backward_images(const hcu_unet_plan *plan, const hcu_unet_tensors *t,
+                              const float *dout, float *dx, int training, int accumulate,
+                              hcu_stream_t stream, const void *images, int images_current);
 
 /* The gated recurrence of RecursiveUnet.forward (hcat/r_unet.py:150-155), n
  * fp32 elements: h = tanh(hp), z = sigmoid(zp), out = h_prev*z + (-1*z*h);

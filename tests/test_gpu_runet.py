@@ -302,3 +302,59 @@ def test_rdcnet_bf16_residual_error_does_not_compound_512x512x24():
     print('RDCNet bf16 vs fp32, residual state y_t relative L2 per step:', ' '.join('%.2e' % e for e in errs))
     assert max(errs) <= 2e-2, errs
     assert errs[-1] <= 3.0 * errs[0] + 1e-3, errs
+
+
+def _step_outputs(net, x):
+    net.zero_grad(set_to_none=True)
+    out = net(x)
+    (out.float() ** 2).mean().backward()
+    torch.cuda.synchronize()
+    return out.detach().cpu(), [p.grad.detach().cpu().clone() for p in net.parameters()]
+
+
+def _fresh_like(net):
+    m = RDCNet(4, 5)
+    m.load_state_dict({k: v.detach().cpu() for k, v in net.state_dict().items()})
+    return m.cuda().train()
+
+
+def _assert_same(a, b):
+    assert torch.equal(a[0], b[0])
+    for ga, gb in zip(a[1], b[1]):
+        assert torch.equal(ga, gb)
+
+
+def test_chain_weight_images_follow_parameter_updates():
+    """The layer chains keep their packed weight images across calls (a
+    recurrence re-lays them once per parameter change, not once per call):
+    after every way the parameters change -- in-place torch ops, this
+    package's Adam, .data writes with invalidate_weight_images(), an eval
+    forward before the training step -- the step equals a fresh module's with
+    the same state, bitwise."""
+    from hcunet_amd import chain as ch
+    from hcunet_amd.optim import Adam
+    g = np.load(os.path.join(GOLD, 'runet_rdc.npz'))
+    torch.manual_seed(3)
+    net = RDCNet(4, 5).cuda().train()
+    x = torch.from_numpy(inputs.make_x(tuple(g['x_shape']))).cuda()
+    _step_outputs(net, x)
+    with torch.no_grad():                       # in-place torch op: version counters move
+        for p in net.parameters():
+            p.mul_(0.9)
+    _assert_same(_step_outputs(net, x), _step_outputs(_fresh_like(net), x))
+    opt = Adam(net.parameters(), lr=1e-2)       # raw-pointer writes: the optimizer's epoch
+    _step_outputs(net, x)
+    opt.step()
+    _assert_same(_step_outputs(net, x), _step_outputs(_fresh_like(net), x))
+    for p in net.parameters():                  # .data bypasses the version counter
+        p.data.mul_(1.1)
+    ch.invalidate_weight_images()
+    _assert_same(_step_outputs(net, x), _step_outputs(_fresh_like(net), x))
+    with torch.no_grad():                       # eval forward lays out the forward images only
+        for p in net.parameters():
+            p.mul_(0.95)
+    net.eval()
+    with torch.no_grad():
+        net(x)
+    net.train()
+    _assert_same(_step_outputs(net, x), _step_outputs(_fresh_like(net), x))
