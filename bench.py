@@ -135,7 +135,8 @@ def load_traffic(kernel, config='2'):
     (profiles/<PROFILE_TAG>_traffic_config<config>.json, written by
     tools/pmc_traffic.py), or None."""
     tab = None
-    for fn in ('%s_traffic_config%s.json' % (PROFILE_TAG, config),):
+    for fn in (('%s_traffic_runet.json' % PROFILE_TAG) if config == 'runet'
+               else ('%s_traffic_config%s.json' % (PROFILE_TAG, config)),):
         if not fn:
             continue
         try:
@@ -402,12 +403,24 @@ def runet_main(args):
             ach, bound, unit, peak = d['bytes'] / d['count'] / avg_s / 1e9, 'hbm', 'GB/s', PEAK_HBM_GBS
         rp_us = rocprof_avg_us(name, 'runet')
         roofline = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
-                    "traffic": None, "kernel": name, "avg_launch_us": avg_s * 1e6,
+                    "traffic": load_traffic(name, 'runet'), "kernel": name, "avg_launch_us": avg_s * 1e6,
                     "flops_per_launch": d['flops'] / d['count'] if d['flops'] > 0 else None,
                     "bytes_per_launch": d['bytes'] / d['count'] if d['bytes'] > 0 else None,
                     "rocprof_avg_launch_us": rp_us,
                     "rocprof_summary": 'profiles/%s_kernel_stats_runet.csv' % PROFILE_TAG if rp_us else None,
                     "launches_per_step": d['count'] / args.steps, "share_of_kernel_time": d['ms'] / total_ms}
+        # the step's roofline from the algorithmic FLOPs and bytes every kernel
+        # declares (bf16 MFMA peak for the bf16 kernels, fp32 for the rest):
+        # sum over kernels of max(bytes / HBM peak, FLOPs / MFMA peak)
+        roof_s = 0.0
+        for k, v in rep.items():
+            pk = PEAK_BF16_MFMA_TFLOPS if ('bf16' in k or k.startswith('bwgrad')) else PEAK_FP32_MFMA_TFLOPS
+            roof_s += max(v['bytes'] / (PEAK_HBM_GBS * 1e9), v['flops'] / (pk * 1e12)) / args.steps
+        step_roof = {"per_kernel_roofline_ms": roof_s * 1e3, "measured_ms": el * 1e3, "frac": roof_s / el,
+                     "flops": sum(v['flops'] for v in rep.values()) / args.steps,
+                     "declared_bytes": sum(v['bytes'] for v in rep.values()) / args.steps,
+                     "note": "sum over the step's kernels of max(declared bytes / 8 TB/s, FLOPs / dense MFMA "
+                             "peak); kernels that declare neither (loss, Adam, copies) count 0"}
         kernels = {"kernel_ms_per_step": total_ms / args.steps,
                    "launches_per_step": sum(v['count'] for v in rep.values()) / args.steps,
                    "algorithmic_tflops_per_step": sum(v['flops'] for v in rep.values()) / args.steps / 1e12,
@@ -416,12 +429,12 @@ def runet_main(args):
                                  key=lambda r: -r['ms_per_step'])[:10]}
     cpu = None
     if not args.no_cpu_baseline:
-        # bounded sample: one fp32 train step of the oracle restatement on a
-        # 128x128x24 tile (same network, same step), scaled per voxel
+        # bounded sample: one fp32 train step of the oracle restatement on the
+        # benched 512x512x24 tile (same network, same step; ~10 s on 16 threads)
         from oracle import runet_oracle as ro, loss_oracle as lo
         threads = max(1, min(16, os.cpu_count() or 1))
         torch.set_num_threads(threads)
-        tile = (128, 128, 24)
+        tile = RUNET_TILE
         st = ro.state_of(RDCNet(4, 5), torch.float32)
         xs = host[0][:, :, :tile[0], :tile[1], :tile[2]].clone()
         t1 = time.perf_counter()
@@ -443,6 +456,8 @@ def runet_main(args):
                                    "memory with async prefetch, bf16 autocast",
                        "final_loss": float(loss.item())},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "layers": layers}
+    if not args.no_kernel_timing:
+        line["step_roofline"] = step_roof
     print(json.dumps(line), flush=True)
 
 

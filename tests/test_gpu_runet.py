@@ -174,15 +174,19 @@ def _rl2(a, b):
     return ((a - b).norm() / max(b.norm().item(), 1e-30)).item()
 
 
-def test_rdcnet_bf16_autocast_relative():
+@pytest.mark.parametrize('tile', [(64, 64, 24), (512, 512, 24)])
+def test_rdcnet_bf16_autocast_relative(tile):
     """BASELINE config 5 runs RDCNet under bf16 autocast; the reference has no
     bf16 path, so this build's distance to the fp32 oracle must be within 1.5x
     of torch's own CPU bf16 autocast of the oracle (output and median
-    gradient relative L2), as tests/test_gpu_bf16.py does for the U-Net."""
+    gradient relative L2), as tests/test_gpu_bf16.py does for the U-Net --
+    on a small tile and on config 5's own 512x512x24 tile (where the dilated
+    convolutions take their sub-lattice tilings; ~40 s of host time)."""
     from oracle import loss_oracle as lo, runet_oracle as ro
+    torch.set_num_threads(16)
     torch.manual_seed(0)
     net = RDCNet(4, 5)
-    shape = (1, 4, 64, 64, 24)
+    shape = (1, 4) + tile
     x = torch.from_numpy(inputs.make_x(shape))
     oshape = (1, 5) + shape[2:]
     mshape = (1, 1) + shape[2:]

@@ -57,6 +57,17 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T
   > $O/${TAG}_profrunet.log 2>&1 || { tail -30 $O/${TAG}_profrunet.log; exit 1; }
 f=$(find $O/${TAG}_profrunet -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_runet.csv
 find $O/${TAG}_profrunet -name '*.csv' -size +20M -delete 2>/dev/null
+# its HBM traffic (FETCH_SIZE / WRITE_SIZE, one pass each; 3 steps profiled)
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetchrunet \
+  -- python3 bench.py --runet --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+  > $O/${TAG}_fetchrunet.log 2>&1 || { tail -20 $O/${TAG}_fetchrunet.log; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_writerunet \
+  -- python3 bench.py --runet --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+  > $O/${TAG}_writerunet.log 2>&1 || { tail -20 $O/${TAG}_writerunet.log; exit 1; }
+python3 tools/pmc_traffic.py $O/${TAG}_fetchrunet $O/${TAG}_writerunet --steps 3 \
+  --out $O/${TAG}_traffic_runet.json > $O/${TAG}_traffic_runet.txt 2>&1 || true
+tail -2 $O/${TAG}_traffic_runet.txt
+find $O/${TAG}_fetchrunet $O/${TAG}_writerunet -name '*.csv' -size +20M -delete 2>/dev/null
 # the bench lines cite profiles/<TAG>_* (bench.py PROFILE_TAG): install this
 # pass's summaries there first (in the box's copy; the results come back via
 # gpurun_out/ and are committed from there)
@@ -66,6 +77,7 @@ for C in 2 3; do
   [ -s $O/${TAG}_traffic_config$C.json ] && cp $O/${TAG}_traffic_config$C.json profiles/${TAG}_traffic_config$C.json
 done
 cp $O/${TAG}_kernel_stats_runet.csv profiles/${TAG}_kernel_stats_runet.csv
+[ -s $O/${TAG}_traffic_runet.json ] && cp $O/${TAG}_traffic_runet.json profiles/${TAG}_traffic_runet.json
 for C in 2 3; do
   timeout -k 10 300 python -u bench.py --config $C --steps 20 --warmup 3 > $O/${TAG}_bench_config$C.json 2> $O/${TAG}_bench_config$C.err \
     || { tail -30 $O/${TAG}_bench_config$C.err; exit 1; }
