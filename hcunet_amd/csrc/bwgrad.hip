@@ -227,9 +227,12 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
     // A rows are 0 (staged as outside), so nothing else is needed.
     lds_barrier();
     for (int p0 = 0; p0 < PT; p0 += 32) {
-      const int pr = p0 + 8 * g + q4;
-      const int ra0 = hvA[pr], ra1 = hvA[pr + 4];
-      const int rg0 = hvG[pr], rg1 = hvG[pr + 4];
+      // voxel rows of this lane's 8 K elements: rows 4g+q4 and 16+4g+q4 of
+      // the 32-voxel step (the same order for both operands), so the 32 lanes
+      // of each ds_read_b64_tr_b16 bank group read 8 consecutive rows
+      const int pr = p0 + 4 * g + q4;
+      const int ra0 = hvA[pr], ra1 = hvA[pr + 16];
+      const int rg0 = hvG[pr], rg1 = hvG[pr + 16];
       shortx8 bf[NS];
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
@@ -491,9 +494,12 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     if (tt + 1 < t_end) load(tt + 1);   // in flight during this tile's MFMAs
     lds_barrier();
     for (int p0 = 0; p0 < PT; p0 += 32) {
-      const int pr = p0 + 8 * g + q4;
-      const int ra0 = hvA[pr], ra1 = hvA[pr + 4];
-      const int rg0 = hvG[pr], rg1 = hvG[pr + 4];
+      // voxel rows of this lane's 8 K elements: rows 4g+q4 and 16+4g+q4 of
+      // the 32-voxel step (the same order for both operands), so the 32 lanes
+      // of each ds_read_b64_tr_b16 bank group read 8 consecutive rows
+      const int pr = p0 + 4 * g + q4;
+      const int ra0 = hvA[pr], ra1 = hvA[pr + 16];
+      const int rg0 = hvG[pr], rg1 = hvG[pr + 16];
       shortx8 bf[NS];
 #pragma unroll
       for (int n = 0; n < NS; ++n) {
@@ -636,8 +642,12 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // the slabs -- measured 7.25 vs 6.63 ms per config-3 step)
   int ntz = cdiv(a.PZ, 16);
   a.TZ = cdiv(a.PZ, ntz);
-  a.PA2 = a.CKA + 8;
-  a.PG2 = a.CKG + 8;
+  // LDS row strides (bf16 elements) with (CK + pad) / 16 odd: 8 consecutive
+  // rows' 32-byte fragments then cover the 64 banks once (was CK + 8, where
+  // e.g. CK = 32, 64 put two of the 8 rows of a read on the same banks)
+  auto pad_of = [](int ck) { return ((16 - ck % 32) % 32 + 32) % 32; };
+  a.PA2 = a.CKA + pad_of(a.CKA);
+  a.PG2 = a.CKG + pad_of(a.CKG);
   // (a 4 x 4 x even-TZ tile -- half the halo image, two blocks per CU on the
   // level-0/1 layers -- measured 7.60-7.66 ms per config-3 step against 6.62:
   // its larger halo share and twice the slabs cost more than the occupancy)
