@@ -642,10 +642,13 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // the slabs -- measured 7.25 vs 6.63 ms per config-3 step)
   int ntz = cdiv(a.PZ, 16);
   a.TZ = cdiv(a.PZ, ntz);
-  // LDS row strides (bf16 elements) with (CK + pad) / 16 odd: 8 consecutive
-  // rows' 32-byte fragments then cover the 64 banks once (was CK + 8, where
-  // e.g. CK = 32, 64 put two of the 8 rows of a read on the same banks)
-  auto pad_of = [](int ck) { return ((16 - ck % 32) % 32 + 32) % 32; };
+  // LDS row strides (bf16 elements) with (CK + pad) / 16 odd for CK >= 32:
+  // 8 consecutive rows' 32-byte fragments then cover the 64 banks once (CK + 8
+  // put two of the 8 rows of a read on the same banks).  CK <= 16 keeps
+  // CK + 8: a smaller image there lets the direct form of RDCNet's dilated
+  // convolutions fit LDS, whose weight gradient then runs without the
+  // sub-lattice split and 7 ms per step slower.
+  auto pad_of = [](int ck) { return ck <= 16 ? 8 : ((16 - ck % 32) % 32 + 32) % 32; };
   a.PA2 = a.CKA + pad_of(a.CKA);
   a.PG2 = a.CKG + pad_of(a.CKG);
   // (a 4 x 4 x even-TZ tile -- half the halo image, two blocks per CU on the
