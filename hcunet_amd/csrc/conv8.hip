@@ -536,9 +536,11 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
     const int HVP = round_up(HV, 16) + 8;
     const long lds = conv8_lds(a, C4, HVP, G);
     const long tiles = (long)a.B * cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz;
-    // two workgroups per CU; <= 12 prefetched elements per thread (16 spills
-    // registers at G = 8)
-    if (lds > 80 * 1024 || HV * C4 > 12 * 256) continue;
+    // two workgroups per CU; <= 12 prefetched elements per thread at G = 8
+    // (16 spills registers there), <= 16 at G <= 4: config 2's d1.c1 input
+    // gradient then takes G = 4 (62 -> 54 us; the step, branch-bound there,
+    // unchanged: 1.958-1.971 vs 1.959-1.965 ms)
+    if (lds > 80 * 1024 || HV * C4 > (G <= 4 ? 16 : 12) * 256) continue;
     a.G8 = G;
     a.TX = TX;
     a.TY = TY;

@@ -1,11 +1,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out; mkdir -p $O
-export HCU_BCONV_TUNE=1
-timeout -k 10 300 python -u bench.py --runet --steps 5 --warmup 2 --no-cpu-baseline > $O/rb_fix.json 2> $O/rb_fix.err || { tail -20 $O/rb_fix.err; exit 1; }
-python3 - <<'PY'
-import json
-d=json.loads(open('gpurun_out/rb_fix.json').read().strip().splitlines()[-1])
-print(d['ms_per_step'], d['kernels']['kernel_ms_per_step'], d['kernels']['launches_per_step'])
-for r in d['kernels']['top']: print(r)
-PY
+for arm in HCU_X=0 HCU_C8_NPF16=1; do
+  echo "== $arm"
+  env $arm timeout -k 10 120 python -u tools/conv_bench.py --reps 20 --only d1.c1,d0.c2 2>&1 | grep -v amdgpu.ids
+done
+bash tools/gpu_abx.sh ab7 2 3 HCU_X=0 HCU_C8_NPF16=1
