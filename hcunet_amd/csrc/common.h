@@ -435,12 +435,6 @@ int launch_bn_bwd_reduce_pool(const float *dP, const float *y, BNCoef coef,
                               int kx, int ky, int kz, float *part, int R,
                               hipStream_t s, int bf = 0);
 // dy = dz*scale + c1*y + c0 in place.
-// bn_bwd_finalize + bn_bwd_apply in one launch (each workgroup re-derives the
-// coefficients from the partial rows; workgroup 0 writes dgamma / dbeta).
-int launch_bn_bwd_finalize_apply(const float *part, int R, int W, int C, int Cs, double count,
-                                 BNCoef coef, float *dgamma, float *dbeta, int training,
-                                 int accumulate, float *dz, const float *y, int64_t nvox,
-                                 hipStream_t s, int bf);
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox,
                         int Cs, hipStream_t s, int bf = 0);
 

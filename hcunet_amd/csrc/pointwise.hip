@@ -783,145 +783,6 @@ bn_bwd_apply_vec_kernel(T *dz, const T *y, BNCoef coef, int64_t nv, int G) {
   }
 }
 
-// BatchNorm backward finalize fused into the apply (the launch-boundary
-// combine): every workgroup first sums the R partial rows of (sum dz,
-// sum dz*xhat) per channel in fp64 -- TPC threads per channel over strided
-// rows, eight rows' loads in flight, then a fixed-order tree -- into its own
-// LDS copy of (scale, c1, c0); workgroup 0 also writes dgamma / dbeta and the
-// c1 / c0 arrays.  Then dy = dz*scale + c1*y + c0 in place over a persistent
-// grid with 16-byte channel vectors.  Deterministic (same rows, same order in
-// every workgroup).
-template <typename T>
-__global__ void __launch_bounds__(256)
-bn_bwd_fin_apply_kernel(T *dz, const T *y, BNCoef coef, const float *part, int R, int W, int C,
-                        int Cs, double count, float *dgamma, float *dbeta, int training,
-                        int accumulate, int64_t nv, int G) {
-  constexpr int N = VN<T>::N;
-  __shared__ double red[2][256];
-  __shared__ float s_sc[512], s_c1[512], s_c0[512];
-  const int tid = threadIdx.x;
-  int TPC = 1;
-  while (TPC * 2 * Cs <= 256 && TPC < 64) TPC *= 2;
-  const int CPP = 256 / TPC, sub = tid % TPC;
-  for (int c0 = 0; c0 < Cs; c0 += CPP) {
-    const int c = c0 + tid / TPC;
-    double a = 0.0, b = 0.0;
-    if (c < C)
-      for (int r0 = sub; r0 < R; r0 += 8 * TPC) {
-        float2 v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int r = r0 + u * TPC;
-          v[u] = r < R ? *reinterpret_cast<const float2 *>(part + ((size_t)r * W + c) * 2) : make_float2(0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          a += (double)v[u].x;
-          b += (double)v[u].y;
-        }
-      }
-    red[0][tid] = a;
-    red[1][tid] = b;
-    __syncthreads();
-    for (int off = TPC / 2; off > 0; off >>= 1) {
-      if (sub < off) {
-        red[0][tid] += red[0][tid + off];
-        red[1][tid] += red[1][tid + off];
-      }
-      __syncthreads();
-    }
-    if (sub == 0 && c < Cs) {
-      float c1v = 0.f, c0v = 0.f, scv = 0.f;
-      if (c < C) {
-        const double db = red[0][tid], dg = red[1][tid];
-        scv = coef.scale[c];
-        if (training) {
-          const double sc = scv, is = coef.invstd[c], mu = coef.mean[c];
-          const double c1 = -sc * is * dg / count;
-          c1v = (float)c1;
-          c0v = (float)(-sc * db / count - c1 * mu);
-        }
-        if (blockIdx.x == 0) {
-          if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)db : (float)db;
-          if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)dg : (float)dg;
-        }
-      }
-      s_sc[c] = scv;
-      s_c1[c] = c1v;
-      s_c0[c] = c0v;
-      if (blockIdx.x == 0) {
-        coef.c1[c] = c1v;
-        coef.c0[c] = c0v;
-      }
-    }
-    __syncthreads();
-  }
-  const int64_t i0 = (int64_t)blockIdx.x * 256 + tid;
-  const int64_t st = (int64_t)gridDim.x * 256;
-  const int c = (int)(i0 % G) * N;
-  float sc[N], c1[N], c0[N];
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    sc[j] = s_sc[c + j];
-    c1[j] = s_c1[c + j];
-    c0[j] = s_c0[c + j];
-  }
-  int64_t i = i0;
-  for (; i + 3 * st < nv; i += 4 * st) {
-    float yy[4][N], d[4][N];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      ldv(y + (i + u * st) * N, yy[u]);
-      ldv(dz + (i + u * st) * N, d[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-#pragma unroll
-      for (int j = 0; j < N; ++j) d[u][j] = fmaf(d[u][j], sc[j], fmaf(c1[j], yy[u][j], c0[j]));
-      stv(dz + (i + u * st) * N, d[u]);
-    }
-  }
-  for (; i < nv; i += st) {
-    float yy[N], d[N];
-    ldv(y + i * N, yy);
-    ldv(dz + i * N, d);
-#pragma unroll
-    for (int j = 0; j < N; ++j) d[j] = fmaf(d[j], sc[j], fmaf(c1[j], yy[j], c0[j]));
-    stv(dz + i * N, d);
-  }
-}
-
-int launch_bn_bwd_finalize_apply(const float *part, int R, int W, int C, int Cs, double count,
-                                 BNCoef coef, float *dgamma, float *dbeta, int training,
-                                 int accumulate, float *dz, const float *y, int64_t nvox,
-                                 hipStream_t s, int bf) {
-  const int N = bf ? 8 : 4;
-  // Each workgroup reads all R x Cs partial pairs before it can apply: only
-  // worth a launch when that is one batch of loads per thread (measured: with
-  // R x Cs up to 8K the fused form was 3-12 % slower per step).
-  if (Cs % N || Cs > 512 || (int64_t)R * Cs > 2048) {   // the separate kernels
-    if (int e = launch_bn_bwd_finalize(part, R, C, Cs, W, count, coef, dgamma, dbeta, training,
-                                       accumulate, s))
-      return e;
-    return launch_bn_bwd_apply(dz, y, coef, nvox, Cs, s, bf);
-  }
-  const int G = Cs / N;
-  const int64_t nv = nvox * G;
-  // persistent: at most 4 workgroups per CU, each re-derives the coefficients once
-  int64_t want = (nv + 1023) / 1024;
-  int grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, 1024));
-  if (256 % G) {
-    const int per = G / std::__gcd(256, G);
-    grid = std::max(per, grid / per * per);
-  }
-  HCU_TIMED(s, "bn_bwd_fin_apply_kernel", 0.0, 0.0,
-            HCU_BF_DISPATCH(bf, bn_bwd_fin_apply_kernel, dim3(grid), dim3(256), 0, s, (T *)dz,
-                            (const T *)y, coef, part, R, W, C, Cs, count, dgamma, dbeta, training,
-                            accumulate, nv, G));
-  HCU_CHECK_LAUNCH();
-  return 0;
-}
-
 int launch_bn_bwd_apply(float *dz, const float *y, BNCoef coef, int64_t nvox, int Cs,
                         hipStream_t s, int bf) {
   {
