@@ -373,3 +373,67 @@ extern "C" int hcu_gather_vectors(float *const *vecs, const int *lens, int n, fl
   HCU_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Channel cat / split of channels-last tensors ([rows][C] with C the padded
+// channel slots of the executor's layout): RDCNet's recurrence concatenates
+// its state with the strided convolution's output and the five dilated
+// branches along channels (hcat/r_unet.py:223, :362).  torch's cat copies
+// each part into a strided slice of the output, and its backward hands every
+// consumer a strided slice that is copied again; here both directions are
+// one launch over 16-byte vectors, coalesced on the full tensor's side.
+namespace hcu {
+constexpr int kCatMax = 8;
+struct CatList {
+  uint4 *p[kCatMax];      // part bases
+  int off[kCatMax + 1];   // first vector of part i in a row; off[n] = row width
+  int n;
+};
+__global__ void __launch_bounds__(256) cl_cat_kernel(const CatList c, uint4 *full, uint32_t nvec, int split) {
+  const uint32_t W = (uint32_t)c.off[c.n];
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nvec; i += gridDim.x * 256u) {
+    const uint32_t row = i / W, j = i - row * W;
+    // part of column j (compile-time indices into the argument block: no
+    // dynamically indexed copy of it)
+    uint4 *base = c.p[0];
+    uint32_t o = 0, w = (uint32_t)c.off[1];
+#pragma unroll
+    for (int q = 1; q < kCatMax; ++q)
+      if (q < c.n && j >= (uint32_t)c.off[q]) {
+        base = c.p[q];
+        o = (uint32_t)c.off[q];
+        w = (uint32_t)(c.off[q + 1] - c.off[q]);
+      }
+    uint4 *pp = base + (size_t)row * w + (j - o);
+    if (split) *pp = full[i];
+    else full[i] = *pp;
+  }
+}
+}  // namespace hcu
+
+extern "C" int hcu_cl_cat(void *const *parts, const int *part_row_bytes, int nparts, void *full, int64_t rows,
+                          int split, void *stream) {
+  if (nparts < 1 || nparts > hcu::kCatMax || !parts || !part_row_bytes || !full || rows < 0)
+    return hcu::fail(1, "hcu_cl_cat: 1..8 parts, non-null buffers");
+  hcu::CatList c{};
+  c.off[0] = 0;
+  for (int i = 0; i < nparts; ++i) {
+    if (!parts[i] || part_row_bytes[i] <= 0 || part_row_bytes[i] % 16 ||
+        reinterpret_cast<uintptr_t>(parts[i]) % 16)
+      return hcu::fail(1, "hcu_cl_cat: parts must be 16-byte aligned with rows of 16-byte multiples");
+    c.p[i] = static_cast<uint4 *>(parts[i]);
+    c.off[i + 1] = c.off[i] + part_row_bytes[i] / 16;
+  }
+  c.n = nparts;
+  if (reinterpret_cast<uintptr_t>(full) % 16) return hcu::fail(1, "hcu_cl_cat: full tensor not 16-byte aligned");
+  const double nv = (double)rows * c.off[nparts];
+  if (nv >= 4294967295.0) return hcu::fail(4, "hcu_cl_cat: more than 2^32 vectors");
+  if (nv == 0) return 0;
+  const uint32_t nvec = (uint32_t)nv;
+  hipStream_t s = (hipStream_t)stream;
+  HCU_TIMED(s, split ? "cl_split_kernel" : "cl_cat_kernel", 0.0, 32.0 * nv,
+            HCU_LAUNCH(hcu::cl_cat_kernel, dim3(hcu::layout_grid(nvec)), dim3(256), 0, s, c,
+                       static_cast<uint4 *>(full), nvec, split));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}

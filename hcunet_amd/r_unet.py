@@ -13,8 +13,9 @@ Compute: every Conv3d [+ BatchNorm3d + ReLU] / MaxPool3d / ConvTranspose3d
 sequence between two recurrence points is ONE layer chain
 (hcunet_amd.chain, hcu_chain_* in include/hcunet.h); the gated update of
 RecursiveUnet is a native kernel (hcu_gate_fwd / hcu_gate_bwd).  What is
-left in torch is data movement on the recurrence: the channel cat of the
-input and the state, and RDCNet's residual add.  StackedDilation's dilated
+left in torch is data movement on the recurrence: RecursiveUnet's channel
+cat of the input and the state, RDCNet's residual add and the state's cast
+(RDCNet's two channel cats are hcu_cl_cat launches, cl_cat).  StackedDilation's dilated
 5^3 convolutions whose halo does not fit a workgroup run on their dilation
 sub-lattices (space-to-batch, hcunet_amd/csrc/layout.hip).  Under
 torch.autocast('cuda', torch.bfloat16) (or compute_dtype = torch.bfloat16)
@@ -113,6 +114,49 @@ class _Gate(torch.autograd.Function):
                                            _lib.ptr(dhp), _lib.ptr(dzp), _lib.ptr(dprev), hp.numel(),
                                            _lib.stream_handle(hp.device)), 'gate backward')
         return dhp, dzp, dprev
+
+
+def _cl_cat_call(parts, full, split):
+    n = len(parts)
+    ptrs = (ctypes.c_void_p * n)(*[p.data_ptr() for p in parts])
+    rb = (ctypes.c_int * n)(*[p.shape[-1] * p.element_size() for p in parts])
+    _lib.check(_lib.lib().hcu_cl_cat(ptrs, rb, n, ctypes.c_void_p(full.data_ptr()), full.numel() // full.shape[-1],
+                                     split, _lib.stream_handle(full.device)), 'channel cat')
+
+
+class _ClCat(torch.autograd.Function):
+    """torch.cat(parts, dim=-1) of channels-last chain tensors (hcat/r_unet.py
+    :223, :362 in the executor's layout) in one launch; the backward hands
+    each part its gradient as a contiguous tensor, again in one launch
+    (hcu_cl_cat), instead of strided slices that every consumer copies."""
+
+    @staticmethod
+    def forward(ctx, *parts):
+        parts = [p.contiguous() for p in parts]
+        lead = parts[0].shape[:-1]
+        widths = [p.shape[-1] for p in parts]
+        out = torch.empty(tuple(lead) + (sum(widths),), dtype=parts[0].dtype, device=parts[0].device)
+        _cl_cat_call(parts, out, 0)
+        ctx.lead, ctx.widths = tuple(lead), widths
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g):
+        g = g.contiguous()
+        grads = [torch.empty(ctx.lead + (w,), dtype=g.dtype, device=g.device) for w in ctx.widths]
+        _cl_cat_call(grads, g, 1)
+        return tuple(grads)
+
+
+def cl_cat(parts):
+    """Channel cat of channels-last tensors with 16-byte channel rows (what
+    the chains produce); other inputs go to torch.cat."""
+    p0 = parts[0]
+    ok = 1 <= len(parts) <= 8 and all(
+        p.is_cuda and p.dtype == p0.dtype and p.dim() == p0.dim() and p.shape[:-1] == p0.shape[:-1]
+        and (p.shape[-1] * p.element_size()) % 16 == 0 for p in parts)
+    return _ClCat.apply(*parts) if ok else torch.cat(parts, dim=-1)
 
 
 def _ready(x, what):
@@ -414,8 +458,8 @@ class RDCNet(nn.Module):
         y = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
         trace = getattr(self, '_y_trace', None)   # (tests: y after every recurrence step)
         for t in range(10):
-            h = step(torch.cat((x, y.to(x.dtype)), dim=-1), tr, bf16)
-            y = mix(torch.cat([d(h, tr, bf16) for d in dil], dim=-1), tr, bf16) + y
+            h = step(cl_cat([x, y.to(x.dtype)]), tr, bf16)
+            y = mix(cl_cat([d(h, tr, bf16) for d in dil]), tr, bf16) + y
             if trace is not None:
                 trace.append(y.detach().clone())
         y = _chain(self, self, 'out_cl', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],

@@ -250,6 +250,15 @@ int hcu_gate_fwd(const float *hp, const float *zp, const float *h_prev, float *o
 int hcu_gate_bwd(const float *hp, const float *zp, const float *h_prev, const float *dout, float *dhp,
                  float *dzp, float *dh_prev, int64_t n, hcu_stream_t stream);
 
+/* Channel cat of channels-last tensors ([rows][C], C the padded channel
+ * slots): split = 0 writes full[r] = parts[0][r] ++ parts[1][r] ++ ...,
+ * split = 1 the reverse (the cat's backward: one contiguous gradient per
+ * part).  1..8 parts, 16-byte aligned, part_row_bytes multiples of 16.
+ * Replaces torch.cat(..., dim=1) on RDCNet's recurrence (hcat/r_unet.py:223
+ * cat(x, y) and :362 the StackedDilation cat) and its autograd backward. */
+int hcu_cl_cat(void *const *parts, const int *part_row_bytes, int nparts, void *full, int64_t rows,
+               int split, hcu_stream_t stream);
+
 /* Data-parallel overlap (hcunet_amd/dist.py): with events set, every later  */
 /* hcu_unet_backward on `plan` records ev_decoder on its weight-gradient     */
 /* stream once the decoder's parameter gradients (up_steps, out_conv) are    */

@@ -362,3 +362,28 @@ def test_chain_weight_images_follow_parameter_updates():
         net(x)
     net.train()
     _assert_same(_step_outputs(net, x), _step_outputs(_fresh_like(net), x))
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('widths', [(16, 16), (16, 16, 16, 16, 16), (8, 24, 4, 4)])
+def test_channel_cat_matches_torch_cat(dtype, widths):
+    """hcu_cl_cat (RDCNet's recurrence cats, hcat/r_unet.py:223,362): forward
+    bitwise equal to torch.cat(dim=-1), and each part's gradient bitwise
+    equal to torch.cat's backward (contiguous tensors here)."""
+    from hcunet_amd.r_unet import cl_cat
+    vec = 16 // torch.empty(0, dtype=dtype).element_size()
+    if any(w % vec for w in widths):
+        pytest.skip('rows of 16-byte multiples only')
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device='cpu').manual_seed(7)
+    parts = [torch.randn(1, 37, 29, 11, w, generator=g).to(dtype).to(dev).requires_grad_() for w in widths]
+    ref = [p.detach().clone().requires_grad_() for p in parts]
+    out = cl_cat(parts)
+    want = torch.cat(ref, dim=-1)
+    assert out.dtype == want.dtype and out.shape == want.shape
+    assert torch.equal(out, want)
+    dout = torch.randn(want.shape, generator=g).to(dtype).to(dev)
+    out.backward(dout)
+    want.backward(dout)
+    for p, r in zip(parts, ref):
+        assert p.grad.is_contiguous() and torch.equal(p.grad, r.grad)
