@@ -437,3 +437,82 @@ extern "C" int hcu_cl_cat(void *const *parts, const int *part_row_bytes, int npa
   HCU_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// RDCNet's residual state under bf16 autocast (hcat/r_unet.py:223-225): the
+// block output m (bf16) plus the fp32 state y promotes to fp32, and the next
+// step's cat takes its bf16 cast.  Forward: out = float(m) + y and out_c =
+// bf16(out) (round to nearest even, as torch's cast) in one pass.  Backward:
+// g = g32 + float(gc) (either nullable: a missing one contributes nothing),
+// dy = g, dm = bf16(g) -- the add's and the cast's backward together.
+namespace hcu {
+__global__ void __launch_bounds__(256) resid_fwd_kernel(const uint4 *m, const float4 *y, float4 *out, uint4 *outc,
+                                                        uint32_t nv) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nv; i += gridDim.x * 256u) {
+    float f[8];
+    unpack8(m[i], f);
+    const float4 y0 = y[2 * i], y1 = y[2 * i + 1];
+    f[0] += y0.x; f[1] += y0.y; f[2] += y0.z; f[3] += y0.w;
+    f[4] += y1.x; f[5] += y1.y; f[6] += y1.z; f[7] += y1.w;
+    out[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    out[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+    outc[i] = pack8(f);
+  }
+}
+__global__ void __launch_bounds__(256) resid_bwd_kernel(const float4 *g32, const uint4 *gc, float4 *dy, uint4 *dm,
+                                                        uint32_t nv) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nv; i += gridDim.x * 256u) {
+    float f[8];
+    if (gc) {
+      unpack8(gc[i], f);
+      if (g32) {
+        const float4 a = g32[2 * i], b = g32[2 * i + 1];
+        f[0] = a.x + f[0]; f[1] = a.y + f[1]; f[2] = a.z + f[2]; f[3] = a.w + f[3];
+        f[4] = b.x + f[4]; f[5] = b.y + f[5]; f[6] = b.z + f[6]; f[7] = b.w + f[7];
+      }
+    } else {
+      const float4 a = g32[2 * i], b = g32[2 * i + 1];
+      f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+      f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    }
+    dy[2 * i] = make_float4(f[0], f[1], f[2], f[3]);
+    dy[2 * i + 1] = make_float4(f[4], f[5], f[6], f[7]);
+    dm[i] = pack8(f);
+  }
+}
+}  // namespace hcu
+
+namespace {
+bool al16(const void *p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+}  // namespace
+
+extern "C" int hcu_resid_fwd(const void *m, const float *y, float *out, void *out_c, int64_t n, void *stream) {
+  if (!m || !y || !out || !out_c || n < 0 || n % 8 || !al16(m) || !al16(y) || !al16(out) || !al16(out_c))
+    return hcu::fail(1, "hcu_resid_fwd: non-null 16-byte aligned buffers, n a multiple of 8");
+  if ((double)n / 8 >= 4294967295.0) return hcu::fail(4, "hcu_resid_fwd: too many elements");
+  if (n == 0) return 0;
+  const uint32_t nv = (uint32_t)(n / 8);
+  hipStream_t s = (hipStream_t)stream;
+  HCU_TIMED(s, "resid_fwd_kernel", 0.0, 12.0 * n,
+            HCU_LAUNCH(hcu::resid_fwd_kernel, dim3(hcu::layout_grid(nv)), dim3(256), 0, s,
+                       static_cast<const uint4 *>(m), reinterpret_cast<const float4 *>(y),
+                       reinterpret_cast<float4 *>(out), static_cast<uint4 *>(out_c), nv));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int hcu_resid_bwd(const float *g32, const void *gc, float *dy, void *dm, int64_t n, void *stream) {
+  if ((!g32 && !gc) || !dy || !dm || n < 0 || n % 8 || (g32 && !al16(g32)) || (gc && !al16(gc)) || !al16(dy) ||
+      !al16(dm))
+    return hcu::fail(1, "hcu_resid_bwd: a gradient, 16-byte aligned buffers, n a multiple of 8");
+  if ((double)n / 8 >= 4294967295.0) return hcu::fail(4, "hcu_resid_bwd: too many elements");
+  if (n == 0) return 0;
+  const uint32_t nv = (uint32_t)(n / 8);
+  hipStream_t s = (hipStream_t)stream;
+  HCU_TIMED(s, "resid_bwd_kernel", 0.0, (g32 ? 4.0 : 0.0) * n + (gc ? 2.0 : 0.0) * n + 6.0 * n,
+            HCU_LAUNCH(hcu::resid_bwd_kernel, dim3(hcu::layout_grid(nv)), dim3(256), 0, s,
+                       reinterpret_cast<const float4 *>(g32), static_cast<const uint4 *>(gc),
+                       reinterpret_cast<float4 *>(dy), static_cast<uint4 *>(dm), nv));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}

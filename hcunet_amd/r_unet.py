@@ -14,8 +14,9 @@ sequence between two recurrence points is ONE layer chain
 (hcunet_amd.chain, hcu_chain_* in include/hcunet.h); the gated update of
 RecursiveUnet is a native kernel (hcu_gate_fwd / hcu_gate_bwd).  What is
 left in torch is data movement on the recurrence: RecursiveUnet's channel
-cat of the input and the state, RDCNet's residual add and the state's cast
-(RDCNet's two channel cats are hcu_cl_cat launches, cl_cat).  StackedDilation's dilated
+cat of the input and the state, and the sums autograd forms for tensors
+that feed several chains (RDCNet's channel cats and its residual add + bf16
+cast are native: cl_cat / hcu_cl_cat, resid_add / hcu_resid_fwd, _bwd).  StackedDilation's dilated
 5^3 convolutions whose halo does not fit a workgroup run on their dilation
 sub-lattices (space-to-batch, hcunet_amd/csrc/layout.hip).  Under
 torch.autocast('cuda', torch.bfloat16) (or compute_dtype = torch.bfloat16)
@@ -157,6 +158,47 @@ def cl_cat(parts):
         p.is_cuda and p.dtype == p0.dtype and p.dim() == p0.dim() and p.shape[:-1] == p0.shape[:-1]
         and (p.shape[-1] * p.element_size()) % 16 == 0 for p in parts)
     return _ClCat.apply(*parts) if ok else torch.cat(parts, dim=-1)
+
+
+class _Resid(torch.autograd.Function):
+    """y' = m + y with m the block output in bf16 and y the fp32 residual
+    state (hcat/r_unet.py:223-225 under autocast: the sum promotes to fp32),
+    returned with its bf16 cast (what the next step's cat and the last conv
+    take), in one launch each way (hcu_resid_fwd / hcu_resid_bwd)."""
+
+    @staticmethod
+    def forward(ctx, m, y):
+        m, y = m.contiguous(), y.contiguous()
+        out = torch.empty(y.shape, dtype=torch.float32, device=y.device)
+        outc = torch.empty(y.shape, dtype=m.dtype, device=y.device)
+        _lib.check(_lib.lib().hcu_resid_fwd(_lib.ptr(m), _lib.ptr(y), _lib.ptr(out), _lib.ptr(outc), y.numel(),
+                                            _lib.stream_handle(y.device)), 'residual add')
+        ctx.set_materialize_grads(False)
+        return out, outc
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g32, gc):
+        if g32 is None and gc is None:
+            return None, None
+        ref = g32 if g32 is not None else gc
+        g32 = g32.contiguous().float() if g32 is not None else None
+        gc = gc.contiguous().to(torch.bfloat16) if gc is not None else None
+        dy = torch.empty(ref.shape, dtype=torch.float32, device=ref.device)
+        dm = torch.empty(ref.shape, dtype=torch.bfloat16, device=ref.device)
+        _lib.check(_lib.lib().hcu_resid_bwd(_lib.ptr(g32), _lib.ptr(gc), _lib.ptr(dy), _lib.ptr(dm), dy.numel(),
+                                            _lib.stream_handle(dy.device)), 'residual add backward')
+        return dm, dy
+
+
+def resid_add(m, y):
+    """(m + y, (m + y).to(m.dtype)) for the bf16 block output m and the fp32
+    state y of RDCNet's recurrence; other dtypes go to torch."""
+    if m.dtype == torch.bfloat16 and y.dtype == torch.float32 and m.shape == y.shape and m.is_cuda \
+            and y.is_cuda and m.numel() % 8 == 0:
+        return _Resid.apply(m, y)
+    s = m + y
+    return s, s.to(m.dtype)
 
 
 def _ready(x, what):
@@ -456,14 +498,15 @@ class RDCNet(nn.Module):
         # promotes to fp32); it is rounded to the compute dtype only where it
         # enters a convolution (the cat of :223, out_conv of :226).
         y = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+        yc = y.to(x.dtype)                             # y in the compute dtype (the cat's / out_conv's input)
         trace = getattr(self, '_y_trace', None)   # (tests: y after every recurrence step)
         for t in range(10):
-            h = step(cl_cat([x, y.to(x.dtype)]), tr, bf16)
-            y = mix(cl_cat([d(h, tr, bf16) for d in dil]), tr, bf16) + y
+            h = step(cl_cat([x, yc]), tr, bf16)
+            y, yc = resid_add(mix(cl_cat([d(h, tr, bf16) for d in dil]), tr, bf16), y)
             if trace is not None:
                 trace.append(y.detach().clone())
         y = _chain(self, self, 'out_cl', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],
-                   in_cl=True)(y.to(x.dtype), tr, bf16)
+                   in_cl=True)(yc, tr, bf16)
         # 5 output channels: no bf16 phase-folded ConvTranspose3d tiling; fp32
         return _chain(self, self, 'convt', self.transposed_conv.in_channels,
                       [('convt', self.transposed_conv)])(y, tr, False)

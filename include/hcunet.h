@@ -259,6 +259,13 @@ int hcu_gate_bwd(const float *hp, const float *zp, const float *h_prev, const fl
 int hcu_cl_cat(void *const *parts, const int *part_row_bytes, int nparts, void *full, int64_t rows,
                int split, hcu_stream_t stream);
 
+/* RDCNet's residual state under bf16 autocast (hcat/r_unet.py:223-225):
+ * out = float(m) + y (fp32) and out_c = its bf16 cast, n elements (a
+ * multiple of 8; m, out_c bf16).  The backward writes dy = g32 + float(gc)
+ * and dm = bf16(dy); g32 or gc may be NULL (no contribution). */
+int hcu_resid_fwd(const void *m, const float *y, float *out, void *out_c, int64_t n, hcu_stream_t stream);
+int hcu_resid_bwd(const float *g32, const void *gc, float *dy, void *dm, int64_t n, hcu_stream_t stream);
+
 /* Data-parallel overlap (hcunet_amd/dist.py): with events set, every later  */
 /* hcu_unet_backward on `plan` records ev_decoder on its weight-gradient     */
 /* stream once the decoder's parameter gradients (up_steps, out_conv) are    */

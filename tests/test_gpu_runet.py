@@ -387,3 +387,34 @@ def test_channel_cat_matches_torch_cat(dtype, widths):
     want.backward(dout)
     for p, r in zip(parts, ref):
         assert p.grad.is_contiguous() and torch.equal(p.grad, r.grad)
+
+
+@pytest.mark.parametrize('use', ['both', 'cast', 'fp32'])
+def test_residual_add_matches_torch(use):
+    """hcu_resid_fwd/bwd (RDCNet's residual under autocast, hcat/r_unet.py
+    :223-225): m (bf16) + y (fp32) and its bf16 cast bitwise equal to torch's
+    promoting add and .to(), and so are the gradients of m and y with either
+    or both outputs used."""
+    from hcunet_amd.r_unet import resid_add
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device='cpu').manual_seed(11)
+    m = torch.randn(1, 33, 21, 13, 16, generator=g).to(torch.bfloat16).to(dev).requires_grad_()
+    y = torch.randn(1, 33, 21, 13, 16, generator=g).to(dev).requires_grad_()
+    m2, y2 = m.detach().clone().requires_grad_(), y.detach().clone().requires_grad_()
+    s, sc = resid_add(m, y)
+    t = m2 + y2
+    tc = t.to(torch.bfloat16)
+    assert s.dtype == torch.float32 and sc.dtype == torch.bfloat16
+    assert torch.equal(s, t) and torch.equal(sc, tc)
+    d32 = torch.randn(t.shape, generator=g).to(dev)
+    dc = torch.randn(t.shape, generator=g).to(torch.bfloat16).to(dev)
+    if use == 'both':
+        ((s * d32).sum() + (sc.float() * dc.float()).sum()).backward()
+        ((t * d32).sum() + (tc.float() * dc.float()).sum()).backward()
+    elif use == 'cast':
+        sc.backward(dc)
+        tc.backward(dc)
+    else:
+        s.backward(d32)
+        t.backward(d32)
+    assert torch.equal(m.grad, m2.grad) and torch.equal(y.grad, y2.grad)
