@@ -139,6 +139,7 @@ SYMBOLS = [
     ("hcu_cl_cat", _I, [ctypes.POINTER(_VP), ctypes.POINTER(_I), _I, _VP, _I64, _I, _VP]),
     ("hcu_resid_fwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_resid_bwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
+    ("hcu_sum_parts", _I, [ctypes.POINTER(_VP), _I, _VP, _I64, _I, _VP]),
     ("hcu_unet_set_grad_events", _I, [_VP, _VP, _VP, _I]),
     ("hcu_unet_grad_events_live", _I, [_VP]),
     ("hcu_event_create", _I, [ctypes.POINTER(_VP)]),

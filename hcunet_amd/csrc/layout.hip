@@ -516,3 +516,78 @@ extern "C" int hcu_resid_bwd(const float *g32, const void *gc, float *dy, void *
   HCU_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Sum of the gradients of a tensor that feeds several chains (RDCNet: the
+// block input h feeds the five dilated branches, the strided convolution's
+// output x the ten recurrence steps): autograd would add them pairwise, one
+// launch and one rounding per add; here one launch sums n <= 16 of them in
+// fp32 in input order and rounds once.  bf = 1: bf16 elements, else fp32;
+// null inputs contribute nothing.
+namespace hcu {
+constexpr int kSumMax = 16;
+struct SumList {
+  const uint4 *p[kSumMax];
+  int n;
+};
+template <bool BF>
+__global__ void __launch_bounds__(256) sum_parts_kernel(const SumList l, uint4 *out, uint32_t nv) {
+  constexpr int N = BF ? 8 : 4;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nv; i += gridDim.x * 256u) {
+    float acc[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) acc[j] = 0.f;
+    bool first = true;
+#pragma unroll
+    for (int q = 0; q < kSumMax; ++q) {
+      if (q >= l.n || !l.p[q]) continue;
+      const uint4 v = l.p[q][i];
+      float f[N];
+      if constexpr (BF) {
+        unpack8(v, f);
+      } else {
+        f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+        f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc[j] = first ? f[j] : acc[j] + f[j];
+      first = false;
+    }
+    if constexpr (BF) {
+      out[i] = pack8(acc);
+    } else {
+      out[i] = make_uint4(__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]),
+                          __float_as_uint(acc[3]));
+    }
+  }
+}
+}  // namespace hcu
+
+extern "C" int hcu_sum_parts(const void *const *parts, int nparts, void *out, int64_t n, int bf, void *stream) {
+  const int per = bf ? 8 : 4;
+  if (nparts < 1 || nparts > hcu::kSumMax || !parts || !out || n < 0 || n % per || !al16(out))
+    return hcu::fail(1, "hcu_sum_parts: 1..16 inputs, 16-byte aligned, n a multiple of the vector");
+  hcu::SumList l{};
+  int live = 0;
+  for (int i = 0; i < nparts; ++i) {
+    if (parts[i] && !al16(parts[i])) return hcu::fail(1, "hcu_sum_parts: input not 16-byte aligned");
+    l.p[i] = static_cast<const uint4 *>(parts[i]);
+    live += parts[i] != nullptr;
+  }
+  if (!live) return hcu::fail(1, "hcu_sum_parts: no input");
+  l.n = nparts;
+  if ((double)n / per >= 4294967295.0) return hcu::fail(4, "hcu_sum_parts: too many elements");
+  if (n == 0) return 0;
+  const uint32_t nv = (uint32_t)(n / per);
+  hipStream_t s = (hipStream_t)stream;
+  if (bf)
+    HCU_TIMED(s, "sum_parts_kernel", 0.0, 2.0 * n * (live + 1),
+              HCU_LAUNCH(hcu::sum_parts_kernel<true>, dim3(hcu::layout_grid(nv)), dim3(256), 0, s, l,
+                         static_cast<uint4 *>(out), nv));
+  else
+    HCU_TIMED(s, "sum_parts_kernel", 0.0, 4.0 * n * (live + 1),
+              HCU_LAUNCH(hcu::sum_parts_kernel<false>, dim3(hcu::layout_grid(nv)), dim3(256), 0, s, l,
+                         static_cast<uint4 *>(out), nv));
+  HCU_CHECK_LAUNCH();
+  return 0;
+}

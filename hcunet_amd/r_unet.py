@@ -13,10 +13,11 @@ Compute: every Conv3d [+ BatchNorm3d + ReLU] / MaxPool3d / ConvTranspose3d
 sequence between two recurrence points is ONE layer chain
 (hcunet_amd.chain, hcu_chain_* in include/hcunet.h); the gated update of
 RecursiveUnet is a native kernel (hcu_gate_fwd / hcu_gate_bwd).  What is
-left in torch is data movement on the recurrence: RecursiveUnet's channel
-cat of the input and the state, and the sums autograd forms for tensors
-that feed several chains (RDCNet's channel cats and its residual add + bf16
-cast are native: cl_cat / hcu_cl_cat, resid_add / hcu_resid_fwd, _bwd).  StackedDilation's dilated
+left in torch is RecursiveUnet's channel cat of the input and the state;
+RDCNet's recurrence glue is native: the channel cats (cl_cat, hcu_cl_cat),
+the residual add with its bf16 cast (resid_add, hcu_resid_fwd / _bwd) and
+the gradient sums of the tensors read by several chains (fan,
+hcu_sum_parts).  StackedDilation's dilated
 5^3 convolutions whose halo does not fit a workgroup run on their dilation
 sub-lattices (space-to-batch, hcunet_amd/csrc/layout.hip).  Under
 torch.autocast('cuda', torch.bfloat16) (or compute_dtype = torch.bfloat16)
@@ -199,6 +200,43 @@ def resid_add(m, y):
         return _Resid.apply(m, y)
     s = m + y
     return s, s.to(m.dtype)
+
+
+class _Fan(torch.autograd.Function):
+    """One tensor handed to k consumers (k views); the backward sums their
+    gradients in one launch (hcu_sum_parts: fp32 accumulation in consumer
+    order, one rounding) instead of autograd's k - 1 pairwise adds."""
+
+    @staticmethod
+    def forward(ctx, t, k):
+        ctx.set_materialize_grads(False)
+        return tuple(t.view_as(t) for _ in range(k))
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, *gs):
+        live = [g for g in gs if g is not None]
+        if len(live) <= 1:
+            return (live[0] if live else None), None
+        ref = live[0]
+        if ref.dtype not in (torch.bfloat16, torch.float32) or any(g.dtype != ref.dtype for g in live):
+            return sum(live[1:], live[0]), None
+        gs = [g.contiguous() if g is not None else None for g in gs]
+        out = torch.empty(ref.shape, dtype=ref.dtype, device=ref.device)
+        ptrs = (ctypes.c_void_p * len(gs))(*[g.data_ptr() if g is not None else None for g in gs])
+        _lib.check(_lib.lib().hcu_sum_parts(ptrs, len(gs), _lib.ptr(out), out.numel(),
+                                            1 if ref.dtype == torch.bfloat16 else 0,
+                                            _lib.stream_handle(out.device)), 'gradient sum')
+        return out, None
+
+
+def fan(t, k):
+    """k uses of t whose gradients are summed in one launch (_Fan); plain
+    repetition where no gradient flows or the shape does not fit."""
+    if k < 2 or k > 16 or not (torch.is_grad_enabled() and t.requires_grad and t.is_cuda) \
+            or t.dtype not in (torch.bfloat16, torch.float32) or t.numel() % 8:
+        return (t,) * k
+    return _Fan.apply(t, k)
 
 
 def _ready(x, what):
@@ -500,9 +538,10 @@ class RDCNet(nn.Module):
         y = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
         yc = y.to(x.dtype)                             # y in the compute dtype (the cat's / out_conv's input)
         trace = getattr(self, '_y_trace', None)   # (tests: y after every recurrence step)
+        xs = fan(x, 10)
         for t in range(10):
-            h = step(cl_cat([x, yc]), tr, bf16)
-            y, yc = resid_add(mix(cl_cat([d(h, tr, bf16) for d in dil]), tr, bf16), y)
+            h = fan(step(cl_cat([xs[t], yc]), tr, bf16), len(dil))
+            y, yc = resid_add(mix(cl_cat([d(hi, tr, bf16) for d, hi in zip(dil, h)]), tr, bf16), y)
             if trace is not None:
                 trace.append(y.detach().clone())
         y = _chain(self, self, 'out_cl', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],

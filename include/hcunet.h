@@ -266,6 +266,12 @@ int hcu_cl_cat(void *const *parts, const int *part_row_bytes, int nparts, void *
 int hcu_resid_fwd(const void *m, const float *y, float *out, void *out_c, int64_t n, hcu_stream_t stream);
 int hcu_resid_bwd(const float *g32, const void *gc, float *dy, void *dm, int64_t n, hcu_stream_t stream);
 
+/* out = parts[0] + parts[1] + ... (n elements, fp32 accumulation in input
+ * order, one rounding; bf = 1: bf16 tensors, else fp32; NULL parts skipped;
+ * at most 16).  The gradient of a tensor read by several chains (RDCNet:
+ * hcat/r_unet.py:223-225,362), which autograd would sum pairwise. */
+int hcu_sum_parts(const void *const *parts, int nparts, void *out, int64_t n, int bf, hcu_stream_t stream);
+
 /* Data-parallel overlap (hcunet_amd/dist.py): with events set, every later  */
 /* hcu_unet_backward on `plan` records ev_decoder on its weight-gradient     */
 /* stream once the decoder's parameter gradients (up_steps, out_conv) are    */

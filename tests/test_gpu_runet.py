@@ -418,3 +418,23 @@ def test_residual_add_matches_torch(use):
         s.backward(d32)
         t.backward(d32)
     assert torch.equal(m.grad, m2.grad) and torch.equal(y.grad, y2.grad)
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_fan_gradient_sum(dtype):
+    """hcu_sum_parts behind fan(): the k consumers' gradients summed in fp32
+    in consumer order and rounded once (bitwise equal to that sum in torch),
+    unused consumers skipped."""
+    from hcunet_amd.r_unet import fan
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device='cpu').manual_seed(5)
+    t = torch.randn(1, 17, 19, 13, 16, generator=g).to(dtype).to(dev).requires_grad_()
+    ws = [torch.randn(t.shape, generator=g).to(dtype).to(dev) for _ in range(6)]
+    outs = fan(t, 7)
+    assert len(outs) == 7 and all(torch.equal(o, t) for o in outs)
+    loss = sum((o.float() * w.float()).sum() for o, w in zip(outs, ws))   # outs[6] unused
+    loss.backward()
+    acc = ws[0].float()
+    for w in ws[1:]:
+        acc = acc + w.float()
+    assert t.grad.dtype == dtype and torch.equal(t.grad, acc.to(dtype))
