@@ -2438,16 +2438,20 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
   int cur = 0;
   if (int e = c.alloc(cur)) return e;
   tag(std::string("chain"), "bwd");
-  if (p.out_cl) {   // dout is already in the layout (and the precision) of the gradient slots
-    HCU_HIP(hipMemcpyAsync(c.buf(cur), dout, (size_t)p.outd.vox() * p.outd.Cs * es, hipMemcpyDeviceToDevice, s));
-  } else if (int e = launch_to_cl(dout, c.buf(cur), p.B, p.outd.C, p.outd.Cs, p.outd.vox() / p.B, s, bf,
-                                  HCU_F32)) {
-    return e;
-  }
+  // out_cl: dout is already in the layout (and the precision) of the gradient
+  // slots, and the last op (a Conv3d without BatchNorm) only reads its output
+  // gradient, so it reads the caller's tensor in place (a chain's backward
+  // runs on `s` alone: every read is ordered before the caller's next use of
+  // that memory on `s`).
+  if (!p.out_cl)
+    if (int e = launch_to_cl(dout, c.buf(cur), p.B, p.outd.C, p.outd.Cs, p.outd.vox() / p.B, s, bf, HCU_F32))
+      return e;
   bool pre = false;   // buf(cur) already holds d(pre-BatchNorm y) of op i
   for (int i = n - 1; i >= 0; --i) {
     const ChainOp &o = p.chain[i];
     const ChainAct &a = in[i];
+    // the output gradient of op i
+    float *dY = p.out_cl && i == n - 1 ? const_cast<float *>(dout) : c.buf(cur);
     const bool need_dA = i > 0 || dx != nullptr;
     const ChainOp *pr = i > 0 ? &p.chain[i - 1] : nullptr;
     if (o.kind == HCU_CHAIN_CONV) {
@@ -2470,7 +2474,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
         float *dys = c.fptr(c.sc, p.sub_off[1]), *dxs = c.fptr(c.sc, p.sub_off[2]);
         const int sd[3] = {L.sub_in.X, L.sub_in.Y, L.sub_in.Z}, so[3] = {L.sub_out.X, L.sub_out.Y, L.sub_out.Z};
         tag(L.name, "wgrad");
-        if (int e = launch_s2b(c.buf(cur), nullptr, nullptr, dys, p.B, L.out.X, L.out.Y, L.out.Z, L.out.Cs, es,
+        if (int e = launch_s2b(dY, nullptr, nullptr, dys, p.B, L.out.X, L.out.Y, L.out.Z, L.out.Cs, es,
                                L.L3, so, s))
           return e;
         if (int e = conv_backward(c, L, c.fptr(c.sv, o.xs_off), nullptr, nullptr, dys, cur,
@@ -2480,7 +2484,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
           if (int e = launch_b2s(dxs, dA, p.B, L.in.X, L.in.Y, L.in.Z, L.in.Cs, es, L.L3, sd, s)) return e;
       } else {
         const ConvLayer *bnl = (pr && pr->kind == HCU_CHAIN_CONV && pr->bn_relu) ? &pr->conv : nullptr;
-        if (int e = conv_backward(c, L, a.x, a.sc, a.sh, c.buf(cur), cur, dA, accumulate, bnl, training, &done))
+        if (int e = conv_backward(c, L, a.x, a.sc, a.sh, dY, cur, dA, accumulate, bnl, training, &done))
           return e;
       }
       if (!need_dA) continue;
