@@ -306,14 +306,30 @@ def runet_main(args):
     bf16 autocast, loss = cross_entropy(out[:, :1], pixel) + MSELoss(out[:, 2:])
     then Adam; the input tiles come from pinned host memory, copied to the GPU
     on a side stream while the previous step computes (a ring of two device
-    buffers).  One step = one tile."""
+    buffers).  One step = one tile per GPU.
+
+    Multi-GPU (BASELINE config 5 names 8 GPUs; launched like the U-Net, one
+    process per GPU under torch.distributed.run): the tiles shard by rank
+    (rank r draws its own tile stream), the parameters are broadcast once
+    from rank 0 and the gradients averaged by hcunet_amd.dist.allreduce_gradients
+    (one collective over the flat gradient buffer the layer chains fill)
+    before the optimizer step (/root/reference/tests/r_unet_test.py:37-56
+    trains one model on such tiles); value = tiles of all ranks / max-over-
+    ranks time (weak scaling)."""
     import hcat.loss as hl
     from hcat.r_unet import RDCNet
-    device = torch.device('cuda', 0)
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
     torch.manual_seed(0)
     model = RDCNet(4, 5).to(device).train()
+    hcunet_amd.dist.broadcast_parameters(model)
     opt = hcunet_amd.optim.Adam(model.parameters(), lr=1e-3)
-    g = torch.Generator().manual_seed(11)
+    g = torch.Generator().manual_seed(11 + 7919 * rank)
     n_host = 4
     host = [((torch.randint(0, 65536, (1, 4) + RUNET_TILE, generator=g).float() / 65536 - 0.5) / 0.5)
             .pin_memory() for _ in range(n_host)]
@@ -348,22 +364,32 @@ def runet_main(args):
             loss = hl.cross_entropy(out[:, 0:1], mask, pwl, method='pixel') + hl.MSELoss(out[:, 2:], vec)
         freed[slot].record(torch.cuda.current_stream(device))
         loss.backward()
+        hcunet_amd.dist.allreduce_gradients(model)
         opt.step()
         state['i'] = i + 1
         return loss
 
+    def sync():
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(device)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    torch.cuda.synchronize(device)
+    sync()
     el = (time.perf_counter() - t0) / args.steps
-    vox = RUNET_TILE[0] * RUNET_TILE[1] * RUNET_TILE[2]
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    vox = world * RUNET_TILE[0] * RUNET_TILE[1] * RUNET_TILE[2]
     roofline = kernels = None
     layers = None
-    if not args.no_kernel_timing:
+    if not args.no_kernel_timing and world == 1:
         _lib.lib().hcu_timing_enable(args.steps * 2048)
         _lib.lib().hcu_timing_detail(1)
         hcunet_amd.chain.TAG_CHAINS = True
@@ -428,7 +454,7 @@ def runet_main(args):
                                    "launches_per_step": v['count'] / args.steps} for k, v in rep.items()),
                                  key=lambda r: -r['ms_per_step'])[:10]}
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         # bounded sample: one fp32 train step of the oracle restatement on the
         # benched 512x512x24 tile (same network, same step; ~10 s on 16 threads)
         from oracle import runet_oracle as ro, loss_oracle as lo
@@ -448,17 +474,21 @@ def runet_main(args):
                "sample": "1 train step (fwd+loss+bwd, no optimizer) of the oracle restatement of RDCNet "
                          "(torch CPU fp32, %d threads) on a %s tile: %.2f s" % (threads, 'x'.join(map(str, tile)), tt)}
     line = {"metric": "training voxels/sec (fwd+bwd+step), r_unet.py RDCNet, 512x512x24 tiles",
-            "value": vox / el, "unit": "voxels/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "value": vox / el, "unit": "voxels/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": el * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16", "data": "synthetic",
             "config": {"workload": "config 5: RDCNet(4, 5) train step (10 recurrent RDCBlock steps, "
                                    "stacked dilations 1..5), B=1, 512x512x24x4 tiles from pinned host "
                                    "memory with async prefetch, bf16 autocast",
+                       "global_batch": world, "per_gpu_batch": 1, "parallelism": "dp%d" % world,
                        "final_loss": float(loss.item())},
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels, "layers": layers}
-    if not args.no_kernel_timing:
+    if not args.no_kernel_timing and world == 1:
         line["step_roofline"] = step_roof
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -538,6 +568,16 @@ def main():
         elapsed = float(t.item())
     final_loss = float(loss.item())
     ms_per_step = elapsed / args.steps * 1e3
+    # host cost of ONE step enqueued onto an idle, synchronised queue (no
+    # backpressure from earlier steps): the median of 7 such steps.  If this
+    # approaches ms_per_step the step is host-bound on this box.
+    idle_enq = []
+    for _ in range(7):
+        sync()
+        t1 = time.perf_counter()
+        step()
+        idle_enq.append(time.perf_counter() - t1)
+    sync()
     vox = world * B * TILE[0] * TILE[1] * TILE[2] * args.steps
     value = vox / elapsed
 
@@ -617,7 +657,8 @@ def main():
                            "global_batch": B * world, "per_gpu_batch": B,
                            "input_dtype": args.input_dtype,
                            "parallelism": "dp%d" % world, "final_loss": final_loss,
-                           "host_enqueue_ms_per_step": t_enq / args.steps * 1e3},
+                           "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
+                           "host_enqueue_idle_ms": statistics.median(idle_enq) * 1e3},
                 "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
                 "tiling": tiling}
         # SURVEY §8d per-layer roofline of the whole step (sum over layers of

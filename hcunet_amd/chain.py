@@ -381,7 +381,8 @@ class _ChainFunction(torch.autograd.Function):
         L = _lib.lib()
         if TAG_CHAINS:
             L.hcu_timing_prefix(chain.name.encode())
-        images, level = plan.images_for(_weight_key(chain), dev)
+        wkey = _weight_key(chain)
+        images, level = plan.images_for(wkey, dev)
         with torch.cuda.device(dev):
             _lib.check(L.hcu_chain_forward_images(plan.handle, ctypes.byref(t), 1 if training else 0,
                                                   _lib.stream_handle(dev), ctypes.c_void_p(images.data_ptr()),
@@ -390,6 +391,7 @@ class _ChainFunction(torch.autograd.Function):
         if TAG_CHAINS:
             L.hcu_timing_prefix(b'')
         ctx.chain, ctx.plan, ctx.training, ctx.bf16 = chain, plan, training, bf16
+        ctx.weight_key = wkey
         ctx.save_for_backward(x, saved)
         return out
 
@@ -399,6 +401,14 @@ class _ChainFunction(torch.autograd.Function):
         x, saved = ctx.saved_tensors
         chain, plan = ctx.chain, ctx.plan
         dev = x.device
+        # the backward reads the plan's weight images: they must still be the
+        # ones its forward used (a later forward of the same plan after a
+        # parameter change re-laid them; stock torch raises on the in-place
+        # modification of a saved weight here too)
+        if plan.image_key != ctx.weight_key:
+            raise RuntimeError('hcunet_amd: a parameter of chain %r was modified (or another forward of '
+                               'the chain ran with other weights) between its forward and its backward'
+                               % chain.name)
         if chain.out_cl:   # the gradient slots' layout and precision
             dout = dout.contiguous().to(torch.bfloat16 if ctx.bf16 else torch.float32)
         else:

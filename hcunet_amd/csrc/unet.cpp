@@ -2424,7 +2424,7 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
 }
 
 int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, const float *dout, float *dx,
-                           int training, int accumulate, hipStream_t s, const void *images = nullptr,
+                           int training, int accumulate, hipStream_t s, void *images = nullptr,
                            int images_current = 0) {
   Ctx c{p, *t, s, (char *)t->saved, (char *)t->scratch, t->params, t->grads};
   if (images) c.wi = (char *)images - p.img_lo;
@@ -2655,7 +2655,7 @@ int hcu_chain_forward_images(const hcu_unet_plan *p, const hcu_unet_tensors *t, 
 }
 
 int hcu_chain_backward_images(const hcu_unet_plan *p, const hcu_unet_tensors *t, const float *dout, float *dx,
-                              int training, int accumulate, hcu_stream_t stream, const void *images,
+                              int training, int accumulate, hcu_stream_t stream, void *images,
                               int images_current) {
   if (!p || !p->is_chain) return fail(HCU_ERR_INVALID, "not a chain plan");
   if (!t || !dout || !t->grads || !t->params || !t->saved || !t->scratch)

@@ -172,14 +172,28 @@ def allreduce_gradients(module, group=None, bn_stats=True):
         elif stats:
             torch.cat([t.reshape(-1) for t in stats], out=tail)
     else:
-        buf = torch.cat([p.grad.reshape(-1) for p in params] + [t.reshape(-1) for t in stats])
+        F = _flat_grads(params)
+        if F is not None and not stats:
+            # the layer chains' models (RDCNet, RecursiveUnet without running
+            # statistics, hcunet_amd.chain.FlatParams): every .grad is a view
+            # of one flat buffer in parameter order -- reduced in place
+            _reduce(F, group, world)
+            return
+        if F is not None:
+            buf = torch.cat([F] + [t.reshape(-1) for t in stats])
+        else:
+            buf = torch.cat([p.grad.reshape(-1) for p in params] + [t.reshape(-1) for t in stats])
     _reduce(buf, group, world)
     off = G.numel() if flat_ok else 0
     if not flat_ok:
-        for p in params:
-            k = p.numel()
-            p.grad.copy_(buf[off:off + k].view_as(p.grad))
-            off += k
+        if F is not None:
+            F.copy_(buf[:F.numel()])
+            off = F.numel()
+        else:
+            for p in params:
+                k = p.numel()
+                p.grad.copy_(buf[off:off + k].view_as(p.grad))
+                off += k
     if native:
         _stats_move(stats, buf[off:], unpack=True)   # one launch
         return
@@ -187,6 +201,24 @@ def allreduce_gradients(module, group=None, bn_stats=True):
         k = t.numel()
         t.copy_(buf[off:off + k].view_as(t))
         off += k
+
+
+def _flat_grads(params):
+    """The gradients as ONE flat tensor when every .grad is a contiguous
+    view of one storage, in parameter order without gaps (what
+    hcunet_amd.chain.FlatParams attaches), else None."""
+    g0 = params[0].grad
+    if g0.dtype != torch.float32:
+        return None
+    st, base, off = g0.untyped_storage().data_ptr(), g0.data_ptr(), 0
+    for p in params:
+        g = p.grad
+        if g.dtype != torch.float32 or not g.is_contiguous() or g.untyped_storage().data_ptr() != st \
+                or g.data_ptr() != base + 4 * off:
+            return None
+        off += g.numel()
+    return torch.empty(0, dtype=torch.float32, device=g0.device).set_(
+        g0.untyped_storage(), g0.storage_offset(), (off,), (1,))
 
 
 def _allreduce_overlapped(eng, buf, n_grads, stats, ranges, ev, group, world):
@@ -248,6 +280,10 @@ def broadcast_parameters(module, src=0, group=None):
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src=src, group=group)
+    # the writes above go through .data (no version-counter bump): packed
+    # weight images a chain kept from an earlier forward are stale now
+    from .chain import invalidate_weight_images
+    invalidate_weight_images()
     if os.environ.get('HCU_DP_OVERLAP', '1') != '0' and hasattr(module, 'engine') \
             and next(module.parameters()).is_cuda:
         prepare_overlap(module)

@@ -156,7 +156,8 @@ def cl_cat(parts):
     the chains produce); other inputs go to torch.cat."""
     p0 = parts[0]
     ok = 1 <= len(parts) <= 8 and all(
-        p.is_cuda and p.dtype == p0.dtype and p.dim() == p0.dim() and p.shape[:-1] == p0.shape[:-1]
+        p.is_cuda and p.device == p0.device and p.dtype == p0.dtype and p.dim() == p0.dim()
+        and p.shape[:-1] == p0.shape[:-1]
         and (p.shape[-1] * p.element_size()) % 16 == 0 for p in parts)
     return _ClCat.apply(*parts) if ok else torch.cat(parts, dim=-1)
 

@@ -233,13 +233,14 @@ int hcu_chain_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, con
  * were written), 1 = the buffer holds the forward images of the current
  * parameters (an eval forward wrote it), 2 = forward and input-gradient
  * images (a training forward wrote it).  The backward must be given the
- * buffer its forward used. */
+ * buffer its forward used; after an eval-mode forward (images_current < 2)
+ * it writes the input-gradient images into that buffer, so it is not const. */
 size_t hcu_chain_weight_image_bytes(const hcu_unet_plan *plan);
 int hcu_chain_forward_images(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
                              hcu_stream_t stream, void *images, int images_current);
 int hcu_chain_backward_images(const hcu_unet_plan *plan, const hcu_unet_tensors *t,
                               const float *dout, float *dx, int training, int accumulate,
-                              hcu_stream_t stream, const void *images, int images_current);
+                              hcu_stream_t stream, void *images, int images_current);
 
 /* The gated recurrence of RecursiveUnet.forward (hcat/r_unet.py:150-155), n
  * fp32 elements: h = tanh(hp), z = sigmoid(zp), out = h_prev*z + (-1*z*h);

@@ -257,3 +257,96 @@ def test_dp_reduces_recursive_unet_batchnorm_statistics():
     for n in r0:
         np.testing.assert_array_equal(r0[n], r1[n])
         np.testing.assert_allclose(r0[n], (g0[n] + g1[n]) / 2, rtol=1e-6, atol=1e-7, err_msg=n)
+
+
+RDC_SHAPE = (2, 4, 24, 24, 10)   # two tiles: one per rank (config 5 shards tiles by rank)
+
+
+def _rdc_loss(out, rank):
+    from oracle import loss_oracle as lo
+    oshape = tuple(out.shape)
+    ms = (RDC_SHAPE[0], 1) + oshape[2:]
+    sl = slice(rank, rank + 1)
+    mask = torch.from_numpy(inputs.make_mask(ms)[sl]).float()
+    pwl = torch.from_numpy(inputs.make_pwl(ms)[sl])
+    vec = torch.from_numpy(inputs.make_x((RDC_SHAPE[0], 3) + oshape[2:], seed=4)[sl] * 0.5)
+    return lo.cross_entropy(out[:, 0:1], mask, pwl, method='pixel') + lo.MSELoss(out[:, 2:], vec)
+
+
+def _rdc_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hcat.r_unet import RDCNet
+        import hcunet_amd
+        from oracle import runet_oracle as ro
+        torch.manual_seed(rank)              # different init per rank
+        m = RDCNet(4, 5)
+        hcunet_amd.dist.broadcast_parameters(m)
+        sd = {k: v.numpy().copy() for k, v in m.state_dict().items()}
+        st = ro.state_of(m, torch.float32)
+        x = torch.from_numpy(inputs.make_x(RDC_SHAPE)[rank:rank + 1])
+        _rdc_loss(ro.rdcnet_forward(st, x), rank).backward()
+        local = {n: st[n].grad.clone() for n, _ in m.named_parameters()}
+        # the production layout of the layer chains (hcunet_amd.chain.FlatParams):
+        # every .grad a view of one flat buffer in parameter order
+        n_all = sum(p.numel() for p in m.parameters())
+        G = torch.zeros(n_all)
+        off = 0
+        for n, p in m.named_parameters():
+            p.grad = G[off:off + p.numel()].view_as(p)
+            p.grad.copy_(local[n])
+            off += p.numel()
+        calls = []
+        real = dist.all_reduce
+
+        def counting_all_reduce(*a, **k):
+            calls.append((a[0].numel(), a[0].data_ptr() == G.data_ptr()))
+            return real(*a, **k)
+        dist.all_reduce = counting_all_reduce
+        try:
+            hcunet_amd.dist.allreduce_gradients(m)
+        finally:
+            dist.all_reduce = real
+        q.put((rank, sd, {n: p.grad.numpy().copy() for n, p in m.named_parameters()},
+               {n: g.numpy().copy() for n, g in local.items()}, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_rdcnet_tiles_sharded_by_rank():
+    """BASELINE config 5 data-parallel (bench.py --runet under torchrun): one
+    RDCNet tile per rank, parameters broadcast from rank 0, the gradients
+    averaged by ONE in-place collective over the flat gradient buffer the
+    layer chains fill -- every rank ends with the mean of the per-tile oracle
+    gradients (the reference's training pattern, tests/r_unet_test.py:37-56,
+    per tile)."""
+    import numpy as np
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rdc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, sd, red, local, calls = q.get(timeout=300)
+        res[r] = (sd, red, local, calls)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (sd0, red0, loc0, calls0), (sd1, red1, loc1, calls1) = res[0], res[1]
+    n_params = sum(v.size for v in loc0.values())
+    assert calls0 == calls1 == [(n_params, True)]   # one collective, in place on the flat buffer
+    from hcat.r_unet import RDCNet
+    torch.manual_seed(0)
+    ref = RDCNet(4, 5).state_dict()
+    for k in sd0:
+        np.testing.assert_array_equal(sd0[k], sd1[k], err_msg=k)
+        np.testing.assert_array_equal(sd0[k], ref[k].numpy(), err_msg=k)
+    for n in red0:
+        assert not np.array_equal(loc0[n], loc1[n]), n      # the two tiles differ
+        np.testing.assert_array_equal(red0[n], red1[n], err_msg=n)
+        np.testing.assert_allclose(red0[n], (loc0[n] + loc1[n]) / 2, rtol=1e-6, atol=1e-9, err_msg=n)

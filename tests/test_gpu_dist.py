@@ -181,3 +181,93 @@ def _check(res, n_coll, loc, n_params=None):
         if lrs0 is not None:
             np.testing.assert_allclose(rs0[k], (lrs0[k] + lrs1[k]) / 2, rtol=1e-6, atol=1e-9, err_msg=k)
     return n_params
+
+
+from tests.test_dist_gloo import RDC_SHAPE  # noqa: E402  (one RDCNet tile per rank)
+
+
+def _rdc_worker(rank, world, port, q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hcat.r_unet import RDCNet
+        import hcunet_amd
+        from oracle import runet_oracle as ro
+        from tests.test_dist_gloo import _rdc_loss
+        torch.manual_seed(rank)                  # different init per rank
+        m = RDCNet(4, 5).cuda().train()
+        xr = torch.from_numpy(inputs.make_x(RDC_SHAPE)[rank:rank + 1])
+        # a step BEFORE the broadcast: the chains keep packed weight images of
+        # this rank's own initial weights, which the broadcast must invalidate
+        (m(xr.cuda()).float() ** 2).mean().backward()
+        hcunet_amd.dist.broadcast_parameters(m)
+        m.zero_grad(set_to_none=True)
+        sd = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        out = m(xr.cuda())
+        import hcat.loss as hl
+        oshape = tuple(out.shape)
+        ms = (RDC_SHAPE[0], 1) + oshape[2:]
+        sl = slice(rank, rank + 1)
+        mask = torch.from_numpy(inputs.make_mask(ms)[sl]).cuda()
+        pwl = torch.from_numpy(inputs.make_pwl(ms)[sl]).cuda()
+        vec = torch.from_numpy(inputs.make_x((RDC_SHAPE[0], 3) + oshape[2:], seed=4)[sl] * 0.5).cuda()
+        (hl.cross_entropy(out[:, 0:1], mask, pwl, method='pixel') + hl.MSELoss(out[:, 2:], vec)).backward()
+        torch.cuda.synchronize()
+        local = {n: p.grad.detach().cpu().numpy().copy() for n, p in m.named_parameters()}
+        calls = []
+        real = dist.all_reduce
+
+        def counting(*a, **k):
+            calls.append(a[0].numel())
+            return real(*a, **k)
+        dist.all_reduce = counting
+        try:
+            hcunet_amd.dist.allreduce_gradients(m)
+        finally:
+            dist.all_reduce = real
+        torch.cuda.synchronize()
+        # the oracle on this rank's tile, from the broadcast parameters
+        ref = RDCNet(4, 5)
+        ref.load_state_dict(sd)
+        st = ro.state_of(ref, torch.float32)
+        _rdc_loss(ro.rdcnet_forward(st, xr), rank).backward()
+        oracle = {n: st[n].grad.numpy().copy() for n, _ in m.named_parameters()}
+        q.put((rank, {k: v.numpy() for k, v in sd.items()}, local,
+               {n: p.grad.detach().cpu().numpy() for n, p in m.named_parameters()}, calls, oracle))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_rdcnet_on_gpu_tiles_sharded_by_rank():
+    """Config 5 data-parallel on the native path, two gloo ranks on one GPU:
+    each rank trains RDCNet on its own tile after a step taken BEFORE the
+    broadcast (so the chains' cached weight images hold that rank's own
+    initial weights and must be invalidated by broadcast_parameters); its
+    native gradients equal the oracle's on its tile from rank 0's parameters,
+    and ONE collective leaves both ranks with their mean."""
+    import numpy as np
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rdc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, *rest = q.get(timeout=240)
+        res[r] = rest
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (sd0, loc0, red0, calls0, or0), (sd1, loc1, red1, calls1, or1) = res[0], res[1]
+    n_params = sum(v.size for v in loc0.values())
+    assert calls0 == calls1 == [n_params]
+    for k in sd0:
+        np.testing.assert_array_equal(sd0[k], sd1[k], err_msg=k)
+    for loc, orc, r in ((loc0, or0, 0), (loc1, or1, 1)):
+        for n, g in orc.items():
+            assert _rel(loc[n], g) <= 1e-3, (r, n, _rel(loc[n], g))
+    for n in red0:
+        np.testing.assert_array_equal(red0[n], red1[n], err_msg=n)
+        np.testing.assert_allclose(red0[n], (loc0[n] + loc1[n]) / 2, rtol=1e-6, atol=1e-9, err_msg=n)

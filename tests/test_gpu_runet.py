@@ -362,18 +362,29 @@ def test_chain_weight_images_follow_parameter_updates():
         net(x)
     net.train()
     _assert_same(_step_outputs(net, x), _step_outputs(_fresh_like(net), x))
+    # a second forward with other weights before the first one's backward:
+    # the backward would read the new weight images -- it raises instead
+    net.zero_grad(set_to_none=True)
+    out1 = net(x)
+    with torch.no_grad():
+        for p in net.parameters():
+            p.mul_(1.01)
+    net(x)
+    with pytest.raises(RuntimeError, match='modified'):
+        (out1.float() ** 2).mean().backward()
 
 
-@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize('widths', [(16, 16), (16, 16, 16, 16, 16), (8, 24, 4, 4)])
+@pytest.mark.parametrize('dtype,widths', [
+    (dt, w) for dt in (torch.bfloat16, torch.float32) for w in ((16, 16), (16, 16, 16, 16, 16))] + [
+    (torch.float32, (8, 24, 4, 4)), (torch.bfloat16, (8, 24, 8, 16))])
 def test_channel_cat_matches_torch_cat(dtype, widths):
     """hcu_cl_cat (RDCNet's recurrence cats, hcat/r_unet.py:223,362): forward
     bitwise equal to torch.cat(dim=-1), and each part's gradient bitwise
-    equal to torch.cat's backward (contiguous tensors here)."""
+    equal to torch.cat's backward (contiguous tensors here; rows of 16-byte
+    multiples, narrow parts included)."""
     from hcunet_amd.r_unet import cl_cat
     vec = 16 // torch.empty(0, dtype=dtype).element_size()
-    if any(w % vec for w in widths):
-        pytest.skip('rows of 16-byte multiples only')
+    assert all(w % vec == 0 for w in widths)
     dev = torch.device('cuda', 0)
     g = torch.Generator(device='cpu').manual_seed(7)
     parts = [torch.randn(1, 37, 29, 11, w, generator=g).to(dtype).to(dev).requires_grad_() for w in widths]

@@ -148,8 +148,14 @@ def check_adam(m, spec, p64, p32, frac=2e-3, lr=1e-3):
         # of that step is not determined by fp32 arithmetic (the reference's
         # fp32 step differs from fp64 there too): only determined entries count
         g64 = p64['grads'][n].double()
-        noise = (p32['grads'][n].double() - g64).abs().max().item()
-        diff &= g64.abs() > 8.0 * noise
+        # per-element noise: the fp32 reference's own error at that entry,
+        # floored at its mean over the tensor
+        e32 = (p32['grads'][n].double() - g64).abs()
+        determined = g64.abs() > 8.0 * torch.maximum(e32, e32.mean())
+        # the check must not pass vacuously: at most 10 % of a tensor excluded
+        if g64.numel() >= 32:
+            assert determined.double().mean().item() >= 0.90, (n, determined.double().mean().item())
+        diff &= determined
         bad = diff.double().mean().item()
         assert bad <= frac, (n, bad)
 
