@@ -216,8 +216,21 @@ def check(code, what=""):
     raise RuntimeError(msg)
 
 
+_raw_stream = getattr(torch._C, '_cuda_getCurrentRawStream', None)
+
+
 def stream_handle(device=None):
-    """hipStream_t of torch's current stream on `device`."""
+    """hipStream_t of torch's current stream on `device` (the raw pointer,
+    without building a torch.cuda.Stream object: host time per call)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, torch.device):
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+        else:
+            idx = torch.device(device).index
+            idx = idx if idx is not None else torch.cuda.current_device()
+        return ctypes.c_void_p(_raw_stream(idx))
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 

@@ -36,9 +36,19 @@ inline ChainRec &chain_rec() {
   static thread_local ChainRec r;
   return r;
 }
+// Host-side cost accounting (HCU_HOST_PROF=1, diagnostics only; timing.cpp
+// prints the per-call averages at exit): 0 kernel launches, 1 other HIP calls
+// through HCU_HIP, 2/3 whole hcu_unet_forward / hcu_unet_backward calls.
+bool host_prof_on();
+double host_now_us();
+void host_prof_add(int k, double us);
+void host_prof_snap(double snap_us[2], long snap_n[2]);
+void host_prof_call(int f, const double snap_us[2], const long snap_n[2], double total_us);
 template <typename F, typename... Args>
 inline void launch_ggl(F kernel, const dim3 &grid, const dim3 &block, uint32_t shmem, hipStream_t st,
                        Args... args) {
+  const bool hp = host_prof_on();
+  const double t0 = hp ? host_now_us() : 0.0;
   ChainRec &r = chain_rec();
   if (r.ev && st == r.s) {
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, nullptr, r.ev, 0, args...);
@@ -46,6 +56,7 @@ inline void launch_ggl(F kernel, const dim3 &grid, const dim3 &block, uint32_t s
   } else {
     hipLaunchKernelGGL(kernel, grid, block, shmem, st, args...);
   }
+  if (hp) host_prof_add(0, host_now_us() - t0);
 }
 #define HCU_LAUNCH(...) ::hcu::launch_ggl(__VA_ARGS__)
 
@@ -169,7 +180,10 @@ int fail(int code, const std::string &msg);
 
 #define HCU_HIP(expr)                                                            \
   do {                                                                           \
+    const bool hp__ = ::hcu::host_prof_on();                                     \
+    const double t__ = hp__ ? ::hcu::host_now_us() : 0.0;                        \
     hipError_t e__ = (expr);                                                     \
+    if (hp__) ::hcu::host_prof_add(1, ::hcu::host_now_us() - t__);               \
     if (e__ != hipSuccess)                                                       \
       return ::hcu::fail(3, std::string(#expr) + ": " + hipGetErrorString(e__)); \
   } while (0)

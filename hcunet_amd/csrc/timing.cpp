@@ -6,6 +6,7 @@
 #include "common.h"
 #include "timing.h"
 #include "../../include/hcunet.h"
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -30,6 +31,66 @@ size_t g_next = 0;
 }  // namespace
 
 bool timing_on() { return g_on; }
+
+// ---- HCU_HOST_PROF=1: host time of kernel launches, other HIP calls and the
+// whole forward / backward enqueue (diagnostics; printed to stderr at exit)
+namespace {
+struct HostProf {
+  // [0] launches, [1] other HIP calls (all calls); per steady-state call of
+  // the forward / backward (from the 6th on): its launches and HIP calls
+  double us[4] = {0, 0, 0, 0};
+  long n[4] = {0, 0, 0, 0};
+  double in_us[2][3] = {{0, 0, 0}, {0, 0, 0}};   // [fwd|bwd][launch, hip, total]
+  long in_n[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  long seen[2] = {0, 0};
+  ~HostProf() {
+    if (n[2] + n[3] == 0) return;
+    const char *what[4] = {"kernel launches", "other HIP calls", "hcu_unet_forward", "hcu_unet_backward"};
+    for (int k = 0; k < 4; ++k)
+      fprintf(stderr, "[hcu host] %-18s %8ld calls %10.1f us total %7.2f us/call\n", what[k], n[k], us[k],
+              n[k] ? us[k] / n[k] : 0.0);
+    const char *ph[2] = {"forward", "backward"};
+    for (int f = 0; f < 2; ++f) {
+      const long c = in_n[f][2];
+      if (!c) continue;
+      fprintf(stderr,
+              "[hcu host] steady %s (%ld calls): %.1f us per call; launches %.1f per call, %.1f us; "
+              "other HIP calls %.1f per call, %.1f us\n",
+              ph[f], c, in_us[f][2] / c, (double)in_n[f][0] / c, in_us[f][0] / c, (double)in_n[f][1] / c,
+              in_us[f][1] / c);
+    }
+  }
+};
+HostProf g_hp;
+const bool g_hp_on = [] {
+  const char *e = getenv("HCU_HOST_PROF");
+  return e && e[0] == '1';
+}();
+}  // namespace
+bool host_prof_on() { return g_hp_on; }
+double host_now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void host_prof_add(int k, double us) {
+  g_hp.us[k] += us;
+  g_hp.n[k] += 1;
+}
+// snapshot at the start of a forward (f = 0) / backward (1); returns a token
+void host_prof_call(int f, const double snap_us[2], const long snap_n[2], double total_us) {
+  if (++g_hp.seen[f] <= 5) return;
+  for (int k = 0; k < 2; ++k) {
+    g_hp.in_us[f][k] += g_hp.us[k] - snap_us[k];
+    g_hp.in_n[f][k] += g_hp.n[k] - snap_n[k];
+  }
+  g_hp.in_us[f][2] += total_us;
+  g_hp.in_n[f][2] += 1;
+}
+void host_prof_snap(double snap_us[2], long snap_n[2]) {
+  for (int k = 0; k < 2; ++k) {
+    snap_us[k] = g_hp.us[k];
+    snap_n[k] = g_hp.n[k];
+  }
+}
 
 void timing_set_tag(const char *tag) {
   if (g_on) g_tag = (g_prefix.empty() ? std::string() : g_prefix + ":") + (tag ? tag : "");

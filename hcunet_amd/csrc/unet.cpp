@@ -765,8 +765,13 @@ int build_plan(hcu_unet_plan &p) {
   }
   if (p.Co > 4) return fail(HCU_ERR_UNSUPPORTED, "out_channels > 4 is not supported yet");
   {
-    // HCU_NCX=0: the separate channels-last pass ahead of the first conv (A/B)
-    static const bool ncx_on = !(getenv("HCU_NCX") && getenv("HCU_NCX")[0] == '0');
+    // The first convolution reads the NCXYZ volume itself in fp32 plans; bf16
+    // plans keep the separate channels-last pass (to_cl_vox) ahead of it: the
+    // NCXYZ gather issues one 4-byte load per channel plane and element, and
+    // config 3 ran 6.345-6.349 ms/step with it against 6.269-6.275 without
+    // (interleaved, round 6).  HCU_NCX=0 / 1 forces either (A/B).
+    static const int ncx_env = getenv("HCU_NCX") ? (getenv("HCU_NCX")[0] == '1' ? 1 : 0) : -1;
+    const bool ncx_on = ncx_env >= 0 ? ncx_env == 1 : p.es == 4;
     const GConvArgs &f = p.dc1[0].fwd;
     const bool conv8_ok = f.use_conv8 && f.ICs == 4 && p.es == 4;
     const bool bconv_ok = f.use_bconv && f.CK == (p.es == 2 ? 8 : 4) && f.NPF > 0 && f.ksplit == 1 && f.nph <= 1;
@@ -1480,8 +1485,25 @@ static int enqueue_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, in
   return HCU_OK;
 }
 
+static int unet_forward_impl(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
+                             hcu_stream_t stream);
 int hcu_unet_forward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
                      hcu_stream_t stream) {
+  const double t0 = host_prof_on() ? host_now_us() : 0.0;
+  double su[2];
+  long sn[2];
+  if (host_prof_on()) host_prof_snap(su, sn);
+  const int rc = unet_forward_impl(plan, t, training, stream);
+  if (host_prof_on()) {
+    const double dt = host_now_us() - t0;
+    host_prof_add(2, dt);
+    host_prof_call(0, su, sn, dt);
+  }
+  return rc;
+}
+
+static int unet_forward_impl(const hcu_unet_plan *plan, const hcu_unet_tensors *t, int training,
+                             hcu_stream_t stream) {
   if (!plan || !t || !t->x || !t->out || !t->params || !t->saved || !t->scratch)
     return fail(HCU_ERR_INVALID, "null argument");
   const hcu_unet_plan &p = *plan;
@@ -1777,9 +1799,19 @@ int hcu_unet_backward(const hcu_unet_plan *plan, const hcu_unet_tensors *t, cons
   }
   key.push_back((uintptr_t)split);
   const bool live = graphs_for(p, true) && !timing_on() ? false : true;
-  return run_graphed(p, key, (hipStream_t)stream, [&](hipStream_t s) {
+  const double t0 = host_prof_on() ? host_now_us() : 0.0;
+  double su[2];
+  long sn[2];
+  if (host_prof_on()) host_prof_snap(su, sn);
+  const int rc = run_graphed(p, key, (hipStream_t)stream, [&](hipStream_t s) {
     return enqueue_backward(p, t, dout, dx, training, accumulate, s, split, live);
   });
+  if (host_prof_on()) {
+    const double dt = host_now_us() - t0;
+    host_prof_add(3, dt);
+    host_prof_call(1, su, sn, dt);
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -9,8 +9,10 @@ tensor gets its own launch.  Optimizer state keeps torch's per-parameter
 layout ('step', 'exp_avg', 'exp_avg_sq'), so state_dict() is compatible.
 """
 import ctypes
+from itertools import chain as _chain_it
 
 import torch
+from torch.optim import optimizer as _topt
 
 from . import _lib
 
@@ -129,8 +131,45 @@ class Adam(torch.optim.Optimizer):
             _lib.stream_handle(p0.device)), 'Adam.step')
         return True
 
-    @torch.no_grad()
+    def zero_grad(self, set_to_none: bool = True):
+        """torch.optim.Optimizer.zero_grad; the set_to_none form without the
+        profiler range when no profiler runs (host time per step)."""
+        if not set_to_none or torch.autograd._profiler_enabled():
+            return super().zero_grad(set_to_none)
+        for group in self.param_groups:
+            for p in group['params']:
+                p.grad = None
+
     def step(self, closure=None):
+        """One Adam step.  torch wraps Optimizer.step in a profiler range and
+        the step hooks; this runs the same hooks, and the range only while a
+        profiler is recording (marked 'hooked' so torch does not wrap it
+        again: ~20 us of host time per step)."""
+        if torch.autograd._profiler_enabled():
+            with torch.autograd.profiler.record_function('Optimizer.step#Adam.step'):
+                return self._hooked_step(closure)
+        return self._hooked_step(closure)
+    step.hooked = True
+
+    def _hooked_step(self, closure):
+        args, kwargs = (self, closure), {}
+        for pre_hook in _chain_it(_topt._global_optimizer_pre_hooks.values(),
+                                  self._optimizer_step_pre_hooks.values()):
+            result = pre_hook(self, args, kwargs)
+            if result is not None:
+                if isinstance(result, tuple) and len(result) == 2:
+                    args, kwargs = result
+                else:
+                    raise RuntimeError('step pre-hook must return None or a tuple of (new_args, new_kwargs)')
+        out = self._step(*args[1:], **kwargs)
+        self._optimizer_step_code()
+        for post_hook in _chain_it(self._optimizer_step_post_hooks.values(),
+                                   _topt._global_optimizer_post_hooks.values()):
+            post_hook(self, args, kwargs)
+        return out
+
+    @torch.no_grad()
+    def _step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():

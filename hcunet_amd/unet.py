@@ -140,9 +140,14 @@ class Unet_Constructor(nn.Module):
         params = eng.params_ready()
         # No gradient can flow (torch.no_grad(), or nothing requires grad): the
         # forward-only plan, which keeps no activations for a backward.
-        fwd_only = not (torch.is_grad_enabled() and
-                        (x.requires_grad or any(p.requires_grad for p in params)))
-        return _UnetFunction.apply(x, eng, bf16, fwd_only, *params)
+        p_grad = any(p.requires_grad for p in params)
+        fwd_only = not (torch.is_grad_enabled() and (x.requires_grad or p_grad))
+        # The parameters are not autograd inputs one by one (82 of them cost
+        # the host ~0.1 ms per step in Function.apply and the engine): their
+        # gradients are written into the flat buffer and attached by the
+        # backward itself (_Engine.grad_target), and ONE empty leaf that
+        # requires grad when any parameter does stands for them in the graph.
+        return _UnetFunction.apply(x, eng, bf16, fwd_only, eng.token(x.device) if p_grad else None)
 
     # -- checkpointing (hcat/unet.py:145-196) --------------------------------
     def save(self, filename, hyperparameters=None):
@@ -407,6 +412,17 @@ class _Engine:
         self.grad_events = None      # (ev_decoder, ev_deep, deep_level) or None
         self.events_recorded = False
         self.grad_version = None     # grad_flat._version right after the last backward
+        # per-parameter views of grad_flat, made once per grad_flat (attaching
+        # a cached view costs the host ~0.4 us, slicing a new one ~5 us: 82
+        # parameters per step)
+        self._grad_views = None
+        self._token = None           # the autograd input that stands for the parameters
+
+    def token(self, dev):
+        t = self._token
+        if t is None or t.device != dev:
+            t = self._token = torch.empty(0, device=dev, requires_grad=True)
+        return t
 
     def check_input(self, x, bf16=False):
         m = self.module_ref
@@ -551,20 +567,27 @@ class _Engine:
                                          device=self.flat.device)
             self.grad_flat = self.comm_flat[:self.flat.numel()]
         G = self.grad_flat
-        base = G.data_ptr()
-        offs = []
-        off = 0
-        for p in params:
-            offs.append(off)
-            off += p.numel()
-        if all(p.grad is None for p in params):
+        views = self._grad_views
+        if views is None or views[0] is not G or len(views[1]) != len(params):
+            offs, vs, off = [], [], 0
+            for p in params:
+                offs.append(off)
+                vs.append(G[off:off + p.numel()].view_as(p))
+                off += p.numel()
+            views = self._grad_views = (G, vs, offs)
+        _, vs, offs = views
+        grads = [p.grad for p in params]
+        if all(g is None for g in grads):
             def finish():
-                for p, o in zip(params, offs):
+                for p, v in zip(params, vs):
                     if p.requires_grad:
-                        p.grad = G[o:o + p.numel()].view_as(p)
+                        p.grad = v
             return G, 0, finish
-        if all(p.grad is not None and p.grad.data_ptr() == base + 4 * o
-               and p.grad.shape == p.shape for p, o in zip(params, offs)):
+        if all(g is v for g, v in zip(grads, vs)):
+            return G, 1, (lambda: None)
+        base = G.data_ptr()
+        if all(g is not None and g.data_ptr() == base + 4 * o and g.shape == p.shape
+               for p, g, o in zip(params, grads, offs)):
             return G, 1, (lambda: None)
         tmp = torch.empty_like(self.flat)
 
@@ -585,9 +608,26 @@ _X_DTYPES = {torch.float32: _lib.HCU_F32, torch.float16: _lib.HCU_F16,
              torch.bfloat16: _lib.HCU_BF16}
 
 
+class _NoCtx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
+
+
+_NO_CTX = _NoCtx()
+
+
+def _on_device(dev):
+    """torch.cuda.device(dev), skipped when dev is already current (the
+    executor creates its side and capture streams on the current device)."""
+    return _NO_CTX if dev.index == torch.cuda.current_device() else torch.cuda.device(dev)
+
+
 class _UnetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, eng, bf16, fwd_only, *params):
+    def forward(ctx, x, eng, bf16, fwd_only, token):
         x = x.contiguous()
         plan = eng.plan(x.shape, bf16, forward_only=fwd_only)
         dev = x.device
@@ -601,7 +641,7 @@ class _UnetFunction(torch.autograd.Function):
         t = eng.tensors(x, out, saved, scratch)
         # The executor's graph-capture and side streams are created on the
         # current device: make it the tensors' device.
-        with torch.cuda.device(dev):
+        with _on_device(dev):
             _lib.check(_lib.lib().hcu_unet_forward(plan.handle, ctypes.byref(t), training,
                                                    _lib.stream_handle(dev)),
                        'Unet_Constructor.forward')
@@ -635,7 +675,7 @@ class _UnetFunction(torch.autograd.Function):
             plan.handle, ev[0] if ev else None, ev[1] if ev else None, ev[2] if ev else 0),
             'Unet_Constructor.backward')
         eng.events_recorded = ev is not None
-        with torch.cuda.device(dev):
+        with _on_device(dev):
             _lib.check(L.hcu_unet_backward(plan.handle, ctypes.byref(t),
                                            ctypes.c_void_p(dout.data_ptr()),
                                            _lib.ptr(dx), ctx.training, accumulate,
@@ -649,4 +689,4 @@ class _UnetFunction(torch.autograd.Function):
         eng.grad_version = eng.grad_flat._version if G is eng.grad_flat else None
         if dx is not None and dx.dtype != x.dtype:
             dx = dx.to(x.dtype)
-        return (dx, None, None, None) + (None,) * len(eng.params)
+        return dx, None, None, None, None

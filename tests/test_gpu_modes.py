@@ -235,11 +235,12 @@ def test_ncxyz_first_layer_matches_layout_pass(tmp_path, bf16, xdt):
     tiles that own each voxel) against the separate channels-last pass
     (HCU_NCX=0): outputs and every gradient bitwise equal over 3 steps (the
     same converted values reach the same MFMAs), the graphed forward
-    included."""
+    included.  (bf16 plans take the layout pass by default: HCU_NCX=1 forces
+    the NCXYZ staging there.)"""
     kw = KW if bf16 == '0' else KW.replace('[8, 16, 32, 64, 128]', '[16, 32, 64, 128]')
     env = {'HCU_TEST_BF16': bf16, 'HCU_TEST_XDT': xdt}
     a = _run(tmp_path, 'lay' + bf16 + xdt, dict(env, HCU_NCX='0'), kw=kw)
-    b = _run(tmp_path, 'ncx' + bf16 + xdt, env, kw=kw)
+    b = _run(tmp_path, 'ncx' + bf16 + xdt, dict(env, HCU_NCX='1'), kw=kw)
     bad = [(it, k, (x - y).abs().max().item())
            for it in range(3) for k, (x, y) in enumerate(zip(a[it], b[it])) if not torch.equal(x, y)]
     assert not bad, bad[:8]
