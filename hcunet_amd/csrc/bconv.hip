@@ -241,7 +241,9 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   const int nb16 = cdiv(Nlog, 16);
   const int ntz = cdiv(a.OZ, 16);
   a.TZ = cdiv(a.OZ, ntz);
-  const long lds_cap = 80 * 1024L;   // (96 / 160 KB measured equal: tools/gpu_bb.sh, ab8)
+  // (96 / 160 KB measured equal on the U-Net layers: tools/gpu_bb.sh, ab8;
+  // HCU_BCONV_LDS_KB for A/B)
+  static const long lds_cap = 1024L * std::max(16, std::min(160, env_int_b("HCU_BCONV_LDS_KB", 80)));
   // Candidate tilings, scored by a simple per-CU time model (cycles):
   //   per (tile, chunk): MFMA S * MPW * NSUB * (16 bf16 | 128 fp32) per wave, staging ~
   //   1200 + 40 per 16-byte element per thread (+ weights when multi-chunk);

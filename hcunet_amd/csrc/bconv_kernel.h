@@ -297,8 +297,15 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // register budget has room for the 20 extra VGPRs (NSUB <= 2, NPF <= 8):
   // measured on MI355X, the NSUB = 4 / NPF = 12 input-gradient variants lost
   // occupancy and ran 40-60 % slower with them.
+  // (NSUB = 1 instances: up to 8 per thread, S <= 32 at NT = 16 -- the 125-tap
+  // kernels of RDCNet at 8 channels per chunk stage their 32 KB chunk images
+  // this way instead of synchronously; slots past the image are skipped, a
+  // uniform branch)
+#ifndef HCU_BCONV_WPR8
+#define HCU_BCONV_WPR8 1
+#endif
   constexpr bool WPOK = NPF > 0 && NPF <= 8 && NSUB <= 2;
-  constexpr int WPR = WPOK ? 5 : 1;
+  constexpr int WPR = WPOK ? ((NSUB == 1 && HCU_BCONV_WPR8) ? 8 : 5) : 1;
   const int n16w = S * 4 * NT;
   const bool wpre = WPOK && nck > 1 && n16w <= 256 * WPR;
   uint4 wpf[WPR];
@@ -309,6 +316,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
         __builtin_amdgcn_make_buffer_rsrc((void *)KA(w), 0, (int)nrec, 0x00020000);
 #pragma unroll
     for (int u = 0; u < WPR; ++u) {
+      if (u > 4 && u * 256 >= n16w) break;   // (uniform: the slots past the image)
       const int idx = tid + u * 256;
       const int n = idx % NT, sg = idx / NT;
       const int off = idx < n16w ? (((chunk * S * 4 + sg) * CoutW + (int)blockIdx.y * NT + n) * 16) : 0x7ffffff0;

@@ -32,6 +32,31 @@
 
 namespace hcu {
 
+#ifdef HCU_BW_PHASES
+// measurement builds only (tools/bw_phases.py): cycles of wave 0 of every
+// block of the all-taps kernel: [0] commit (incl. the wait for the prefetched
+// tile), [1] the two barriers + next-tile load issue, [2] MFMA loop, [3] tiles
+__device__ unsigned long long g_bw_phase[4096 * 4];
+extern "C" int hcu_debug_bw_phases(unsigned long long *out) {
+  static unsigned long long h[4096 * 4];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bw_phase), sizeof h) != hipSuccess) return 3;
+  for (int k = 0; k < 4; ++k) out[k] = 0;
+  for (int i = 0; i < 4096 * 4; ++i) out[i % 4] += h[i];
+  for (auto &x : h) x = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_bw_phase), h, sizeof h) == hipSuccess ? 0 : 3;
+}
+#define BW_MARK(k)                                                 \
+  do {                                                             \
+    const long long t__ = (long long)__builtin_readcyclecounter(); \
+    bw_ph[k] += t__ - bw_t;                                        \
+    bw_t = t__;                                                    \
+  } while (0)
+#else
+#define BW_MARK(k) \
+  do {             \
+  } while (0)
+#endif
+
 __device__ __forceinline__ shortx4 tr_read(const uint16_t *p) {
   typedef short v4s __attribute__((ext_vector_type(4)));
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -308,8 +333,9 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
 // in flight while the current tile's MFMAs run, and a tile costs two LDS-only
 // barriers.  The halo coordinates of every register slot are tile-independent
 // and decoded once.
-template <int MSW, int NS, int NP>
+template <int MSW, int NS, int NPA, int NPG>
 __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
+  static_assert(MSW < 16 || NS == 1, "the all-taps form has one column subtile");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -403,22 +429,26 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     sh[k] = act ? a.a_shift[ci0 + ca * 8 + k] : 0.f;
   }
   // halo coordinates of each register slot: hx << 20 | hy << 10 | hz, -1 unused
-  int hoA[NP], hoG[NP];
+  int hoA[NPA], hoG[NPG];
 #pragma unroll
-  for (int k = 0; k < NP; ++k) {
+  for (int k = 0; k < NPA; ++k) {
     const int v = va0 + k * vsA;
     int q, hz, hx, hy;
     a.fHAZ.divmod(v, q, hz);
     a.fHAY.divmod(q, hx, hy);
     hoA[k] = v < HAV ? (hx << 20) | (hy << 10) | hz : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < NPG; ++k) {
     const int w = vg0 + k * vsG;
+    int q, hz, hx, hy;
     a.fHGZ.divmod(w, q, hz);
     a.fHGY.divmod(q, hx, hy);
     hoG[k] = w < HGV ? (hx << 20) | (hy << 10) | hz : -1;
   }
   const uint16_t *Ab = reinterpret_cast<const uint16_t *>(a.A);
   const uint16_t *Gb = reinterpret_cast<const uint16_t *>(a.G);
-  uint4 ra[NP], rg[NP];
+  uint4 ra[NPA], rg[NPG];
   unsigned oka = 0;
 
   auto load = [&](int tt) {
@@ -433,7 +463,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
       const uint16_t *base = Ab + (size_t)b * a.AX * a.AY * a.AZ * a.ACs + ci0 + ca * 8;
       oka = 0;
 #pragma unroll
-      for (int k = 0; k < NP; ++k) {
+      for (int k = 0; k < NPA; ++k) {
         const int h = hoA[k];
         const int gx = gx0 + (h >> 20), gy = gy0 + ((h >> 10) & 1023), gz = gz0 + (h & 1023);
         const bool ok = h >= 0 && (unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY &&
@@ -448,7 +478,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
       const size_t boff = (size_t)b * a.GX * a.GY * a.GZ * a.GCs + co0 + cg * 8;
       const uint16_t *base = Gb + boff;
 #pragma unroll
-      for (int k = 0; k < NP; ++k) {
+      for (int k = 0; k < NPG; ++k) {
         const int h = hoG[k];
         const int gx = gx0 + (h >> 20), gy = gy0 + ((h >> 10) & 1023), gz = gz0 + (h & 1023);
         // taps_rows: G is the output grid [PX][PY][PZ] (voxels past it are 0)
@@ -463,7 +493,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
   };
   auto commit = [&]() {
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
+    for (int k = 0; k < NPA; ++k) {
       if (hoA[k] < 0) continue;
       uint4 w = ra[k];
       if (act && ((oka >> k) & 1u)) {
@@ -476,7 +506,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
       *reinterpret_cast<uint4 *>(alds + (size_t)(va0 + k * vsA) * RSA + ca * 8) = w;
     }
 #pragma unroll
-    for (int k = 0; k < NP; ++k) {
+    for (int k = 0; k < NPG; ++k) {
       if (hoG[k] < 0) continue;
       const uint4 w = rg[k];
       *reinterpret_cast<uint4 *>(glds + (size_t)(vg0 + k * vsG) * RSG + cg * 8) = w;
@@ -488,11 +518,66 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
   const int t_beg = kbi * tpb_;
   const int t_end = min(total, t_beg + tpb_);
   if (t_beg < t_end) load(t_beg);
+#ifdef HCU_BW_PHASES
+  long long bw_ph[4] = {0, 0, 0, 0};
+  long long bw_t = (long long)__builtin_readcyclecounter();
+#endif
   for (int tt = t_beg; tt < t_end; ++tt) {
     lds_barrier();   // the previous tile's fragment reads are done
+    BW_MARK(1);
     commit();
+    BW_MARK(0);
     if (tt + 1 < t_end) load(tt + 1);   // in flight during this tile's MFMAs
     lds_barrier();
+    BW_MARK(1);
+    if constexpr (MSW >= 16) {
+      // Many row subtiles per wave (the all-taps form): the A fragments run
+      // through a ring of D registers, each read issued D MFMAs ahead of its
+      // use and the next 32-voxel step's first fragments (and its G fragment)
+      // read during the current step's last MFMAs, so the LDS latency stays
+      // hidden behind the MFMA chain (the compiler's own schedule reused one
+      // fragment register and waited for every read: ~3x slower).
+      constexpr int D = 8;
+      const int q = 4 * g + q4;
+      int ra0 = hvA[q], ra1 = hvA[q + 16], rg0 = hvG[q], rg1 = hvG[q + 16];
+      auto rdA = [&](int r0, int r1, int m) {
+        const shortx4 lo = tr_read(alds + r0 + colA[m]);
+        const shortx4 hi = tr_read(alds + r1 + colA[m]);
+        return shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      };
+      auto rdG = [&](int r0, int r1) {
+        const shortx4 lo = tr_read(glds + r0 + colG[0]);
+        const shortx4 hi = tr_read(glds + r1 + colG[0]);
+        return shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      };
+      shortx8 bcur = rdG(rg0, rg1), bnext = bcur;
+      shortx8 fr[D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) fr[d] = rdA(ra0, ra1, d);
+      for (int p0 = 0; p0 < PT; p0 += 32) {
+        // the next step's rows (the last step re-reads its own: valid addresses)
+        const int pn = min(p0 + 32, PT - 32) + q;
+        const int na0 = hvA[pn], na1 = hvA[pn + 16], ng0 = hvG[pn], ng1 = hvG[pn + 16];
+#pragma unroll
+        for (int m = 0; m < MSW; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[m % D], bcur, acc[m][0], 0, 0, 0);
+          if (m + D < MSW)
+            fr[m % D] = rdA(ra0, ra1, m + D);
+          else
+            fr[m % D] = rdA(na0, na1, m + D - MSW);
+          if (m == MSW - D) bnext = rdG(ng0, ng1);
+        }
+        if (do_bias) accb[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bcur, accb[0], 0, 0, 0);
+        bcur = bnext;
+        ra0 = na0;
+        ra1 = na1;
+      }
+      BW_MARK(2);
+#ifdef HCU_BW_PHASES
+      bw_ph[3] += 1;
+#endif
+      continue;
+    }
     for (int p0 = 0; p0 < PT; p0 += 32) {
       // voxel rows of this lane's 8 K elements: rows 4g+q4 and 16+4g+q4 of
       // the 32-voxel step (the same order for both operands), so the 32 lanes
@@ -524,6 +609,12 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     }
   }
 
+#ifdef HCU_BW_PHASES
+  if (MSW >= 16 && tid == 0 && blockIdx.y == 0 && blockIdx.z == 0) {
+    unsigned long long *d = g_bw_phase + (size_t)(blockIdx.x % 4096) * 4;
+    for (int k = 0; k < 4; ++k) d[k] += (unsigned long long)bw_ph[k];
+  }
+#endif
   const size_t slab = (size_t)blockIdx.x * a.Mtot;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
@@ -581,7 +672,13 @@ static int bw_cus() {
   return v;
 }
 
-static int plan_bwgrad_cka(WGradArgs &a, int cka_cap);
+static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps);
+
+// HCU_BW_ALLTAPS=0: split the taps of a many-tap kernel over blocks (A/B)
+static bool alltaps_enabled() {
+  static const bool on = !(getenv("HCU_BW_ALLTAPS") && getenv("HCU_BW_ALLTAPS")[0] == '0');
+  return on;
+}
 
 int plan_bwgrad(WGradArgs &a, int target_blocks) {
   (void)target_blocks;
@@ -590,10 +687,18 @@ int plan_bwgrad(WGradArgs &a, int target_blocks) {
   // channel chunks: A side up to 32 channels, G side up to 64 (16-col
   // subtiles).  (16-channel A chunks measured 7.11 vs 6.63 ms per config-3
   // step; 64-channel ones fit the LDS of almost no layer.)
-  return plan_bwgrad_cka(a, 32);
+  if (alltaps_enabled() && plan_bwgrad_cka(a, 32, true) == 0) return 0;
+  return plan_bwgrad_cka(a, 32, false);
 }
 
-static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
+// alltaps: a kernel with more (tap, channel) rows than one block's 36 row
+// subtiles (RDCNet's 5x5x5 convolutions: 125 taps x 16 channel slots) keeps
+// ALL of them in one block -- 32 row subtiles per wave, the column chunk one
+// 16-column subtile -- so each voxel tile's A halo and G image are staged once
+// for every tap instead of once per tap chunk (the split form re-stages both
+// for each of its 4 tap chunks and ran at ~3-4 % of bf16 MFMA).  Fails (the
+// caller then takes the split form) for any other shape.
+static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
   a.use_bw = 0;
   const int T = a.KX * a.KY * a.KZ;
   // padded operands (zero padding of A, or a cropped ConvTranspose3d output
@@ -609,13 +714,20 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
     const int rows_all = T * a.CKA;                    // all taps of one channel chunk
     const int sub_all = cdiv(rows_all, 16);
     int msw = cdiv(sub_all, 4);
-    if (msw > 9) msw = 9;                              // split the taps over blocks (36 rows each)
-    a.MSW = msw <= 3 ? 3 : (msw <= 5 ? 5 : 9);
-    a.TA = std::min(T, (a.MSW * 4 * 16) / a.CKA);
+    if (alltaps && (msw <= 9 || msw > 32 || a.NSB != 1)) return 1;
+    if (alltaps) {
+      a.MSW = 32;
+      a.TA = T;
+    } else {
+      if (msw > 9) msw = 9;                            // split the taps over blocks (36 rows each)
+      a.MSW = msw <= 3 ? 3 : (msw <= 5 ? 5 : 9);
+      a.TA = std::min(T, (a.MSW * 4 * 16) / a.CKA);
+    }
     if (a.TA < 1) return fail(4, "bwgrad: channel chunk too large");
     a.TG = 1;
     a.ntc = cdiv(T, a.TA);
   } else {
+    if (alltaps) return 1;
     // rows = input channels of one chunk (CKA / 16 subtiles), columns = (tap, co)
     a.CKA = std::min(a.ACs, 64);
     if (a.ACs % a.CKA) a.CKA = (a.ACs % 32 == 0) ? 32 : (a.ACs % 16 == 0 ? 16 : 8);
@@ -648,7 +760,9 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // CK + 8: a smaller image there lets the direct form of RDCNet's dilated
   // convolutions fit LDS, whose weight gradient then runs without the
   // sub-lattice split and 7 ms per step slower.
-  auto pad_of = [](int ck) { return ck <= 16 ? 8 : ((16 - ck % 32) % 32 + 32) % 32; };
+  // The all-taps form reads 8 consecutive voxel rows per lane group: 32-byte
+  // rows (no pad) put them on the 64 banks once.
+  auto pad_of = [&](int ck) { return ck <= 16 ? (alltaps && ck == 16 ? 0 : 8) : ((16 - ck % 32) % 32 + 32) % 32; };
   a.PA2 = a.CKA + pad_of(a.CKA);
   a.PG2 = a.CKG + pad_of(a.CKG);
   // (a 4 x 4 x even-TZ tile -- half the halo image, two blocks per CU on the
@@ -676,9 +790,12 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   const int nti = 2;
   int pick = -1;
   long best_lds = 1L << 40;
+  // (alltaps: one block per CU -- its registers allow no second one -- so
+  // the largest tile that fits the CU's LDS: the smallest halo share)
+  const long lds_cap = alltaps ? 156 * 1024 : 80 * 1024;
   for (int i = t0i; i < nti && pick < 0; ++i) {
     const long l = set_tile(i);
-    if (l <= 80 * 1024) pick = i;
+    if (l <= lds_cap) pick = i;
     else if (l < best_lds) { best_lds = l; pick = -2 - i; }
   }
   if (pick < -1) pick = -2 - pick;
@@ -689,7 +806,7 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // reads little) takes half the Z extent per tile: two resident blocks
   // Config 3 (interleaved A/B, 2 runs): slabs <= 64 KB (d0.c2, u3.c2) 6.50 vs
   // 6.62 ms/step without; <= 160 KB 6.56; <= 640 KB 6.96.
-  if (lds > 80 * 1024 && (long)a.Mtot * a.Ntot * 4 <= 64 * 1024 && a.PZ > 8) {
+  if (!alltaps && lds > 80 * 1024 && (long)a.Mtot * a.Ntot * 4 <= 64 * 1024 && a.PZ > 8) {
     ntz = cdiv(a.PZ, 8);
     a.TZ = cdiv(a.PZ, ntz);
     const int TZh = a.TZ;
@@ -719,6 +836,11 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   const int nA = cdiv(a.HAV, 256 / (a.CKA / 8)), nG = cdiv(a.HGV, 256 / (a.CKG / 8));
   const int np = std::max(nA, nG);
   a.NPA = a.NPG = np <= 8 ? 8 : np <= 16 ? 16 : np <= 32 ? 32 : 0;
+  if (alltaps) {   // the instances of launch_bwgrad's BWT list
+    a.NPA = nA <= 8 ? 8 : nA <= 12 ? 12 : nA <= 20 ? 20 : 0;
+    a.NPG = nG <= 8 ? 8 : 0;
+    if (!a.NPA || !a.NPG || a.CKA > 16) return 1;
+  }
   // One fp32 slab per block: the pipelined kernel hides its loads behind the
   // MFMAs of the same block, so it needs at most two blocks per CU -- fewer
   // blocks, fewer slabs for the finalize to read.
@@ -727,7 +849,7 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap) {
   // The network's first layer (<= 8 input channels) runs last on the branch,
   // after the chain has finished: its grid takes the whole chip (config 3,
   // interleaved A/B, 3 runs: 6.433-6.449 vs 6.455-6.461 ms/step at 224 CUs).
-  const int cus = a.ACs <= 8 ? 256 : bw_cus();
+  const int cus = (a.ACs <= 8 || alltaps) ? 256 : bw_cus();
   long kb = std::max(1L, (long)cus * occ_kb / per);
   kb = std::min(kb, total);
   a.KB = (int)kb;
@@ -752,12 +874,23 @@ int launch_bwgrad(const WGradArgs &a, hipStream_t s) {
                            (double)a.B * a.GX * a.GY * a.GZ * a.GCs);
   bool ok = false;
 #define BWP(MS_, NS_, NP_)                                                                  \
-  if (!ok && a.NPA == NP_) {                                                                \
+  if (!ok && a.NPA == NP_ && a.NPG == NP_) {                                                \
     HCU_TIMED(s, "bwgrad_pipe_kernel<" #MS_ "," #NS_ "," #NP_ ">", fl, by,                    \
-              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_>), grid, dim3(256),         \
+              HCU_LAUNCH((bwgrad_pipe_kernel<MS_, NS_, NP_, NP_>), grid, dim3(256),         \
                                  a.lds_bytes, s, a));                                       \
     ok = true;                                                                              \
   }
+  // all taps of a channel chunk in one block (MSW = 32): the A halo and G tile
+  // are staged once per tile for every tap (plan_bwgrad_cka)
+#define BWT(NPA_, NPG_)                                                                     \
+  if (!ok && a.MSW == 32 && a.NSB == 1 && a.NPA == NPA_ && a.NPG == NPG_) {                 \
+    HCU_TIMED(s, "bwgrad_pipe_kernel<32,1," #NPA_ "," #NPG_ ">", fl, by,                     \
+              HCU_LAUNCH((bwgrad_pipe_kernel<32, 1, NPA_, NPG_>), grid, dim3(256),          \
+                         a.lds_bytes, s, a));                                               \
+    ok = true;                                                                              \
+  }
+  BWT(8, 8) BWT(12, 8) BWT(20, 8)
+#undef BWT
 #define BW(MS_, NS_)                                                                        \
   if (!ok && a.MSW == MS_ && a.NSB <= NS_) {                                                \
     BWP(MS_, NS_, 8) BWP(MS_, NS_, 16) BWP(MS_, NS_, 32)                                    \

@@ -449,3 +449,57 @@ def test_fan_gradient_sum(dtype):
     for w in ws[1:]:
         acc = acc + w.float()
     assert t.grad.dtype == dtype and torch.equal(t.grad, acc.to(dtype))
+
+
+_RDC_CHILD = r'''
+import sys, torch
+sys.path.insert(0, %(root)r)
+import hcat.loss as hl
+from hcat.r_unet import RDCNet
+from oracle import inputs
+torch.manual_seed(0)
+net = RDCNet(4, 5).cuda().train()
+shape = %(shape)r
+x = torch.from_numpy(inputs.make_x(shape)).cuda()
+mshape = (1, 1) + shape[2:]
+mask = torch.from_numpy(inputs.make_mask(mshape)).cuda()
+pwl = torch.from_numpy(inputs.make_pwl(mshape)).cuda()
+vec = torch.from_numpy(inputs.make_x((1, 3) + shape[2:]) * 0.5).cuda()
+with torch.autocast('cuda', dtype=torch.bfloat16):
+    out = net(x)
+    loss = hl.cross_entropy(out[:, 0:1], mask, pwl, method='pixel') + hl.MSELoss(out[:, 2:], vec)
+loss.backward()
+torch.cuda.synchronize()
+torch.save({k: p.grad.detach().cpu() for k, p in net.named_parameters()}, %(out)r)
+'''
+
+
+def _rdc_child(tmp_path, tag, env_extra, shape):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / ('%s.pt' % tag))
+    env = dict(os.environ)
+    env.update(env_extra)
+    r = subprocess.run([sys.executable, '-c', _RDC_CHILD % dict(root=root, out=out, shape=shape)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.parametrize('shape', [(1, 4, 64, 64, 24), (1, 4, 40, 56, 20)])
+def test_rdcnet_bf16_weight_gradient_all_taps_matches_split(tmp_path, shape):
+    """The bf16 weight gradient of RDCNet's 5x5x5 convolutions with all 125
+    taps in one block (each voxel tile staged once, HCU_BW_ALLTAPS default)
+    against the form that splits the taps over 4 blocks (HCU_BW_ALLTAPS=0):
+    the same products summed over other slab partitions, so every gradient
+    tensor agrees to fp32 reassociation of the bf16 products (relative L2
+    <= 1e-4; the dilated branches' tensors are the ones that differ)."""
+    a = _rdc_child(tmp_path, 'all', {'HCU_BW_ALLTAPS': '1'}, shape)
+    b = _rdc_child(tmp_path, 'split', {'HCU_BW_ALLTAPS': '0'}, shape)
+    bad = []
+    for k in a:
+        r = _rl2(a[k], b[k])
+        if not r <= 1e-4:
+            bad.append((k, r))
+    assert not bad, bad
