@@ -351,6 +351,13 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   const bool act = a.in_scale != nullptr;
   uint4 pf[NPFR];
   uint32_t okbits = 0;
+  // the last fetch's buffer resource and per-element byte offsets: the next
+  // channel chunk of the same tile only moves every valid offset by CK
+  // channels (fetch_adv) instead of re-deriving the tile origin and the
+  // element addresses from the LDS copy of the arguments (~1.5 K cycles per
+  // chunk in the deep levels' multi-chunk tiles)
+  __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, 0, 0x00020000);
+  int foff[NPFR];
   // halo of (tile, chunk) -> pf (branch-free: the validity of each element is
   // a mask, invalid elements read offset 0x7ffffff0, outside the buffer -> 0)
   // NCXYZ input (NCX): element u's channels from the planes; the raw loaded
@@ -404,8 +411,19 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
                       ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
+      foff[u] = off;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       okbits |= (uint32_t)ok << u;
+    }
+    frs = rs;
+  };
+  auto fetch_adv = [&]() {   // the next channel chunk of the tile just fetched
+    if constexpr (!NCX) {
+#pragma unroll
+      for (int u = 0; u < NPFR; ++u) {
+        foff[u] += ((okbits >> u) & 1u) ? CK * ES : 0;
+        pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(frs, foff[u], 0, 0));
+      }
     }
   };
   // The block's first halo fetch, from the kernel arguments themselves (the
@@ -439,9 +457,11 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
                       ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
+      foff[u] = off;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
+    frs = rs;
   };
   auto load_coefs = [&]() {
     for (int j = tid; j < NT; j += 256) {
@@ -542,6 +562,12 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   };
 
   floatx4 acc[MPW][NSUB];
+  // fp32 instances with a single (M, N) subtile per wave: the four 16x16x4
+  // MFMAs of a K-step alternate between two accumulators (two dependency
+  // chains: the 40-cycle MFMA latency no longer paces a lone chain at 4 per
+  // K-step), summed once before the epilogue
+  constexpr bool DUAL = ES == 4 && MPW * NSUB == 1;
+  floatx4 acc2[MPW][NSUB];
   auto load_frag = [&](int s, int toff, uint4 (&bfr)[NSUB], uint4 (&afr)[MPW]) {
     const int ss = min(s, S - 1);
 #pragma unroll
@@ -552,6 +578,14 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   };
   auto toff_of = [&](int s) { return toffs[min(s, S - 1) * 4 + g]; };
   auto mfma_frag = [&](const uint4 (&bfr)[NSUB], const uint4 (&afr)[MPW]) {
+    if constexpr (DUAL) {
+      const floatx4 wf = __builtin_bit_cast(floatx4, bfr[0]), xf = __builtin_bit_cast(floatx4, afr[0]);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[0], xf[0], acc[0][0], 0, 0, 0);
+      acc2[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[1], xf[1], acc2[0][0], 0, 0, 0);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[2], xf[2], acc[0][0], 0, 0, 0);
+      acc2[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[3], xf[3], acc2[0][0], 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < MPW; ++j)
 #pragma unroll
@@ -587,6 +621,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // wave stores (its value + bias), see below
   bool need_piv = true;
   auto epilogue = [&](int b, int ox0, int oy0, int oz0) {
+    if constexpr (DUAL) acc[0][0] += acc2[0][0];
     const int OX = KA(OX), OY = KA(OY), OZ = KA(OZ), OCs = KA(OCs);
     const bool interior = ox0 + KA(TX) <= OX && oy0 + KA(TY) <= OY && oz0 + KA(TZ) <= OZ;
     const int sample = KA(SX) * KA(SY) * KA(SZ) * OCs;
@@ -706,7 +741,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
 #pragma unroll
-        for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < NSUB; ++n) acc[j][n] = acc2[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
         lds_barrier();
         if constexpr (NCX) {
@@ -732,7 +767,10 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
           nt = tile + 1;
         }
         if (nt < t_end) {
-          fetch(nt, nc);
+          if (nt == tile)
+            fetch_adv();
+          else
+            fetch(nt, nc);
           if (wpre) wfetch(nc);
         }
         PH_MARK(2);
@@ -753,7 +791,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
 #pragma unroll
       for (int j = 0; j < MPW; ++j)
 #pragma unroll
-        for (int n = 0; n < NSUB; ++n) acc[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < NSUB; ++n) acc[j][n] = acc2[j][n] = floatx4{0.f, 0.f, 0.f, 0.f};
       for (int chunk = cb; chunk < ce; ++chunk) {
         lds_barrier();
         stage_direct(tile, chunk);

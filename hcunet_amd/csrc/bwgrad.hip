@@ -355,11 +355,14 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
   const int t0 = tapc * (a.taps_rows ? a.TA : a.TG);
   const bool bias_block = a.taps_rows && a.bias_row && tapc == 0 && cic == 0;
   const int HAV = a.HAV, HGV = a.HGV, PT = a.PTV;
-  uint16_t *alds = reinterpret_cast<uint16_t *>(smem);          // [HAV][RSA]
-  uint16_t *glds = alds + (size_t)HAV * RSA;                    // [HGV][RSG]
+  // the A image keeps HAZP >= HAZ rows per (hx, hy) column (plan_bwgrad_cka:
+  // the all-taps form pads them so 8 consecutive tile voxels land on 8
+  // different bank groups)
+  const int HAZ = a.HAZP, HAYZ = a.HAY * a.HAZP, HGZ = a.HGZ, HGYZ = a.HGY * a.HGZ;
+  uint16_t *alds = reinterpret_cast<uint16_t *>(smem);          // [HAX*HAY*HAZP][RSA]
+  uint16_t *glds = alds + (size_t)a.HAX * HAYZ * RSA;           // [HGV][RSG]
   int *hvA = reinterpret_cast<int *>(glds + (size_t)HGV * RSG);  // [PT] A row * RSA
   int *hvG = hvA + PT;                                           // [PT] G row * RSG
-  const int HAZ = a.HAZ, HAYZ = a.HAY * a.HAZ, HGZ = a.HGZ, HGYZ = a.HGY * a.HGZ;
 
   for (int p = tid; p < PT; p += 256) {
     int q, lz, lx, ly;
@@ -458,9 +461,14 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
     tile /= a.ntz;
     const int tyi = tile % a.nty, txi = tile / a.nty;
     const int px0 = txi * a.TX, py0 = tyi * a.TY, pz0 = tzi * a.TZ;
+    // buffer loads of one batch sample with 32-bit offsets: an element outside
+    // the operand reads an offset past the buffer (-> 0), no branch per element
     {
       const int gx0 = px0 * a.asx - a.apx, gy0 = py0 * a.asy - a.apy, gz0 = pz0 * a.asz - a.apz;
-      const uint16_t *base = Ab + (size_t)b * a.AX * a.AY * a.AZ * a.ACs + ci0 + ca * 8;
+      const int sampleA = a.AX * a.AY * a.AZ * a.ACs;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(Ab + (size_t)b * sampleA), 0, sampleA * 2, 0x00020000);
+      const int cof = (ci0 + ca * 8) * 2, rowA = a.ACs * 2;
       oka = 0;
 #pragma unroll
       for (int k = 0; k < NPA; ++k) {
@@ -468,15 +476,17 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
         const int gx = gx0 + (h >> 20), gy = gy0 + ((h >> 10) & 1023), gz = gz0 + (h & 1023);
         const bool ok = h >= 0 && (unsigned)gx < (unsigned)a.AX && (unsigned)gy < (unsigned)a.AY &&
                         (unsigned)gz < (unsigned)a.AZ;
-        ra[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (ok) ra[k] = *reinterpret_cast<const uint4 *>(base + (((size_t)gx * a.AY + gy) * a.AZ + gz) * a.ACs);
+        const int off = ok ? ((gx * a.AY + gy) * a.AZ + gz) * rowA + cof : 0x7ffffff0;
+        ra[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         oka |= (ok ? 1u : 0u) << k;
       }
     }
     {
       const int gx0 = px0 * a.gsx - a.gpx, gy0 = py0 * a.gsy - a.gpy, gz0 = pz0 * a.gsz - a.gpz;
-      const size_t boff = (size_t)b * a.GX * a.GY * a.GZ * a.GCs + co0 + cg * 8;
-      const uint16_t *base = Gb + boff;
+      const int sampleG = a.GX * a.GY * a.GZ * a.GCs;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(Gb + (size_t)b * sampleG), 0, sampleG * 2, 0x00020000);
+      const int cof = (co0 + cg * 8) * 2, rowG = a.GCs * 2;
 #pragma unroll
       for (int k = 0; k < NPG; ++k) {
         const int h = hoG[k];
@@ -485,9 +495,8 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
         const bool ok = h >= 0 && (unsigned)gx < (unsigned)a.GX && (unsigned)gy < (unsigned)a.GY &&
                         (unsigned)gz < (unsigned)a.GZ &&
                         (!a.taps_rows || (gx < a.PX && gy < a.PY && gz < a.PZ));
-        const size_t vo = (((size_t)gx * a.GY + gy) * a.GZ + gz) * a.GCs;
-        rg[k] = make_uint4(0u, 0u, 0u, 0u);
-        if (ok) rg[k] = *reinterpret_cast<const uint4 *>(base + vo);
+        const int off = ok ? ((gx * a.GY + gy) * a.GZ + gz) * rowG + cof : 0x7ffffff0;
+        rg[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       }
     }
   };
@@ -503,7 +512,9 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
         for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f);
         w = pack8(f);
       }
-      *reinterpret_cast<uint4 *>(alds + (size_t)(va0 + k * vsA) * RSA + ca * 8) = w;
+      const int h = hoA[k];   // the halo voxel's row of the padded image
+      const int row = ((h >> 20) * a.HAY + ((h >> 10) & 1023)) * HAZ + (h & 1023);
+      *reinterpret_cast<uint4 *>(alds + (size_t)row * RSA + ca * 8) = w;
     }
 #pragma unroll
     for (int k = 0; k < NPG; ++k) {
@@ -783,7 +794,12 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
     a.HAV = a.HAX * a.HAY * a.HAZ;
     a.HGV = a.HGX * a.HGY * a.HGZ;
     a.PTV = a.TX * a.TY * a.TZ;
-    return ((long)a.HAV * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
+    // (all-taps form) rows per (hx, hy) column of the A image: HAZP = TZ mod
+    // 8, so the 8 consecutive tile voxels of a fragment read -- z-runs of TZ
+    // rows, consecutive columns HAZP rows apart -- land on 8 different groups
+    // of 8 banks (32-byte rows)
+    a.HAZP = alltaps ? a.HAZ + ((a.TZ - a.HAZ) % 8 + 8) % 8 : a.HAZ;
+    return ((long)a.HAX * a.HAY * a.HAZP * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
   };
   // the first tile whose image fits two blocks per CU, else the smallest
   const int t0i = 0;   // (starting at the 4 x 8 tile measured equal)
@@ -815,6 +831,7 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
     a.HAV = a.HAX * a.HAY * a.HAZ;
     a.HGV = a.HGX * a.HGY * a.HGZ;
     a.PTV = a.TX * a.TY * TZh;
+    a.HAZP = a.HAZ;
     lds = ((long)a.HAV * a.PA2 + (long)a.HGV * a.PG2) * 2 + 2L * a.PTV * 4;
   }
   if (lds > 160 * 1024) return fail(4, "bwgrad: tile does not fit LDS");
