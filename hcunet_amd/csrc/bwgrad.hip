@@ -27,6 +27,7 @@
 #include "common.h"
 #include "timing.h"
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 
@@ -589,34 +590,65 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
 #endif
       continue;
     }
-    for (int p0 = 0; p0 < PT; p0 += 32) {
-      // voxel rows of this lane's 8 K elements: rows 4g+q4 and 16+4g+q4 of
-      // the 32-voxel step (the same order for both operands), so the 32 lanes
-      // of each ds_read_b64_tr_b16 bank group read 8 consecutive rows
-      const int pr = p0 + 4 * g + q4;
-      const int ra0 = hvA[pr], ra1 = hvA[pr + 16];
-      const int rg0 = hvG[pr], rg1 = hvG[pr + 16];
-      shortx8 bf[NS];
+    // Two A fragments in flight: fragment m + 1 is read while fragment m's
+    // NS MFMAs run, and the next 32-voxel step's G fragments and first A
+    // fragment during the step's last row subtile (the same MFMAs in the same
+    // order per accumulator: bitwise the sums of the plain loop, which waited
+    // for every fragment read before its MFMAs).  With an odd MSW the ring's
+    // slots swap roles from one step to the next (sb), so steps run in pairs.
+    // voxel rows of this lane's 8 K elements: rows 4g+q4 and 16+4g+q4 of the
+    // 32-voxel step (the same order for both operands), so the 32 lanes of
+    // each ds_read_b64_tr_b16 bank group read 8 consecutive rows
+    const int q = 4 * g + q4;
+    int ra0 = hvA[q], ra1 = hvA[q + 16];
+    auto rdA = [&](int r0, int r1, int m) {
+      const shortx4 lo = tr_read(alds + r0 + colA[m]);
+      const shortx4 hi = tr_read(alds + r1 + colA[m]);
+      return shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    auto rdG = [&](int r0, int r1, int n) {
+      const shortx4 lo = tr_read(glds + r0 + colG[n]);
+      const shortx4 hi = tr_read(glds + r1 + colG[n]);
+      return shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    };
+    shortx8 bc[NS], bn[NS], ring[2];
+    {
+      const int rg0 = hvG[q], rg1 = hvG[q + 16];
 #pragma unroll
-      for (int n = 0; n < NS; ++n) {
-        const shortx4 lo = tr_read(glds + rg0 + colG[n]);
-        const shortx4 hi = tr_read(glds + rg1 + colG[n]);
-        bf[n] = shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
+      for (int n = 0; n < NS; ++n) bc[n] = rdG(rg0, rg1, n);
+    }
+    ring[0] = rdA(ra0, ra1, 0);
+    auto step = [&](auto SB, int p0) {
+      constexpr int sb = decltype(SB)::value;
+      const int pn = min(p0 + 32, PT - 32) + q;   // (the last step re-reads its own rows)
+      const int na0 = hvA[pn], na1 = hvA[pn + 16], ng0 = hvG[pn], ng1 = hvG[pn + 16];
 #pragma unroll
       for (int m = 0; m < MSW; ++m) {
-        const shortx4 lo = tr_read(alds + ra0 + colA[m]);
-        const shortx4 hi = tr_read(alds + ra1 + colA[m]);
-        const shortx8 af = shortx8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const shortx8 af = ring[(m + sb) & 1];
+        if (m + 1 < MSW) {
+          ring[(m + 1 + sb) & 1] = rdA(ra0, ra1, m + 1);
+        } else {
+          ring[(m + 1 + sb) & 1] = rdA(na0, na1, 0);
+#pragma unroll
+          for (int n = 0; n < NS; ++n) bn[n] = rdG(ng0, ng1, n);
+        }
 #pragma unroll
         for (int n = 0; n < NS; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[n], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bc[n], acc[m][n], 0, 0, 0);
       }
       if (do_bias) {
 #pragma unroll
         for (int n = 0; n < NS; ++n)
-          accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bf[n], accb[n], 0, 0, 0);
+          accb[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bc[n], accb[n], 0, 0, 0);
       }
+#pragma unroll
+      for (int n = 0; n < NS; ++n) bc[n] = bn[n];
+      ra0 = na0;
+      ra1 = na1;
+    };
+    for (int p0 = 0; p0 < PT; p0 += 64) {
+      step(std::integral_constant<int, 0>{}, p0);
+      if (p0 + 32 < PT) step(std::integral_constant<int, MSW & 1>{}, p0 + 32);
     }
   }
 
