@@ -747,7 +747,10 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
   // padded operands (zero padding of A, or a cropped ConvTranspose3d output
   // as G) are staged as zeros outside their grids
   a.CKA = std::min(a.ACs, cka_cap);
-  if (a.ACs % a.CKA) a.CKA = 8;
+  // (the largest of 32 / 16 / 8 channels that divides ACs: RDCNet's mixing
+  // 1x1 convolution reads 5 parts x 16 = 80 channel slots -- 5 chunks of 16,
+  // not 10 of 8, each of which re-stages the G tile)
+  if (a.ACs % a.CKA) a.CKA = (a.ACs % 16 == 0 && cka_cap >= 16) ? 16 : 8;
   a.CKG = std::min(a.GCs, 64);
   if (a.GCs % a.CKG) a.CKG = (a.GCs % 32 == 0) ? 32 : (a.GCs % 16 == 0 ? 16 : 8);
   const int ncol_tiles_full = a.taps_rows ? cdiv(a.CKG, 16) : 0;
@@ -763,7 +766,9 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
       a.TA = T;
     } else {
       if (msw > 9) msw = 9;                            // split the taps over blocks (36 rows each)
-      a.MSW = msw <= 3 ? 3 : (msw <= 5 ? 5 : 9);
+      // (one row subtile per wave for the 1x1 kernels: 16-32 rows; three
+      // per wave there left 11 of 12 MFMA subtiles of a block on padding)
+      a.MSW = msw <= 1 && !getenv("HCU_BW_MSW3") ? 1 : msw <= 3 ? 3 : (msw <= 5 ? 5 : 9);
       a.TA = std::min(T, (a.MSW * 4 * 16) / a.CKA);
     }
     if (a.TA < 1) return fail(4, "bwgrad: channel chunk too large");
