@@ -36,7 +36,7 @@ from hcunet_amd import _lib  # noqa: E402
 import hcunet_amd.chain  # noqa: E402
 from hcunet_amd import roofline as roofline_mod  # noqa: E402
 
-PROFILE_TAG = 'r05'   # the round whose committed profiles/ summaries bench.py cites
+PROFILE_TAG = 'r06'   # the round whose committed profiles/ summaries bench.py cites
 
 METRIC = "training voxels/sec (fwd+bwd+step), 5-level 3D U-Net, 256×256×16×4 tiles"
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, dense

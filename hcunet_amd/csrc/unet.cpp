@@ -1077,7 +1077,11 @@ int finish_bnbwd(const Ctx &c, const GConvArgs &a, const ConvLayer &bnl, float *
 int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
                   const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
                   const ConvLayer *bnl = nullptr, int training = 1, bool *bn_done = nullptr,
-                  float *colsum = nullptr) {
+                  float *colsum = nullptr, bool wg_late = false);
+
+// The weight-gradient half of conv_backward (forked onto the branch).
+int conv_wgrad(Ctx &c, const ConvLayer &L, const float *A, const float *asc, const float *ash,
+               const float *dy, int dy_slot, int accumulate) {
   tag(L.name, "wgrad");
   if (int e = c.fork()) return e;
   WGradArgs w = L.wg;
@@ -1105,7 +1109,17 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   f.ACs = w.ACs;
   f.accumulate = accumulate;
   if (int e = c.pend_wgf(f)) return e;   // finalized with the next flush (Ctx::slab / end of backward)
-  if (int e = c.read_done(dy_slot)) return e;
+  return c.read_done(dy_slot);
+}
+
+// wg_late: the weight gradient is forked after the input gradient's
+// convolution is enqueued (and before its BatchNorm finalize), so the
+// branch's kernel does not start beside it (HCU_L0_ORDER, level 0 A/B).
+int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
+                  const float *ash, const float *dy, int dy_slot, float *dA, int accumulate,
+                  const ConvLayer *bnl, int training, bool *bn_done, float *colsum, bool wg_late) {
+  if (!wg_late || !dA)
+    if (int e = conv_wgrad(c, L, A, asc, ash, dy, dy_slot, accumulate)) return e;
   if (!dA) return 0;
   tag(L.name, "dgrad");
   GConvArgs a = L.dgrad;
@@ -1116,6 +1130,8 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
   const bool fused = fuse_bnbwd(c, a, bnl);
   if (!fused && colsum) a.stats = colsum;
   if (int e = launch_conv_any(a, c.s)) return e;
+  if (wg_late)
+    if (int e = conv_wgrad(c, L, A, asc, ash, dy, dy_slot, accumulate)) return e;
   if (!fused) return 0;
   tag(bnl->name, "bnbwd");
   if (int e = finish_bnbwd(c, a, *bnl, dA, training, accumulate)) return e;
@@ -1718,8 +1734,9 @@ static int enqueue_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, c
     if (int e = c.alloc(sb)) return e;
     float *A = c.buf(cur), *Bf = c.buf(sb);
     bool done1 = false;
+    static const int l0_order = getenv("HCU_L0_ORDER") ? atoi(getenv("HCU_L0_ORDER")) : 0;
     if (int e = conv_backward(c, c2, c.fptr(c.sv, c1.y_off), b1.scale, b1.shift, A, cur, Bf,
-                              accumulate, &c1, training, &done1))
+                              accumulate, &c1, training, &done1, nullptr, i == 0 && l0_order == 1))
       return e;
     if (!done1)
       if (int e = bn_backward(c, c1, Bf, nullptr, nullptr, training, accumulate)) return e;
