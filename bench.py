@@ -499,6 +499,9 @@ def main():
     ap.add_argument('--config', default='2', choices=sorted(CONFIGS))
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--idle-steps', type=int, default=7,
+                    help='extra single steps enqueued onto an idle queue after the '
+                         'timed region (host_enqueue_idle_ms); 0 in profiling passes')
     ap.add_argument('--fresh-input', action='store_true',
                     help='clone the input every step (data-loader pattern; checks graph re-use)')
     ap.add_argument('--infer', action='store_true',
@@ -572,7 +575,7 @@ def main():
     # backpressure from earlier steps): the median of 7 such steps.  If this
     # approaches ms_per_step the step is host-bound on this box.
     idle_enq = []
-    for _ in range(7):
+    for _ in range(args.idle_steps):
         sync()
         t1 = time.perf_counter()
         step()
@@ -658,7 +661,8 @@ def main():
                            "input_dtype": args.input_dtype,
                            "parallelism": "dp%d" % world, "final_loss": final_loss,
                            "host_enqueue_ms_per_step": t_enq / args.steps * 1e3,
-                           "host_enqueue_idle_ms": statistics.median(idle_enq) * 1e3},
+                           "host_enqueue_idle_ms": (statistics.median(idle_enq) * 1e3
+                                                    if idle_enq else None)},
                 "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
                 "tiling": tiling}
         # SURVEY §8d per-layer roofline of the whole step (sum over layers of

@@ -23,28 +23,28 @@ if [ "$TESTS" = 1 ]; then
 fi
 for C in $CONFIGS; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_prof$C \
-    -- python3 bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
     > $O/${TAG}_prof$C.log 2>&1 || { tail -30 $O/${TAG}_prof$C.log; exit 1; }
   f=$(find $O/${TAG}_prof$C -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_config$C.csv
   echo "rocprof config $C: $(head -3 $O/${TAG}_kernel_stats_config$C.csv | tail -2 | cut -c1-120)"
   # the same bench with the backward on one stream: kernel durations under the
   # conditions of bench.py's serialized HIP-event timing pass
   HCU_SIDE=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_profs$C \
-    -- python3 bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py --config $C --steps 20 --warmup 3 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
     > $O/${TAG}_profs$C.log 2>&1 || { tail -30 $O/${TAG}_profs$C.log; exit 1; }
   f=$(find $O/${TAG}_profs$C -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_serial_config$C.csv
   timeout -k 10 300 rocprofv3 --kernel-trace -d $O/${TAG}_tl$C \
-    -- python3 bench.py --config $C --steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py --config $C --steps 6 --warmup 2 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
     > $O/${TAG}_tl$C.log 2>&1 || { tail -30 $O/${TAG}_tl$C.log; exit 1; }
   db=$(find $O/${TAG}_tl$C -name '*.db' | head -1)
   python3 tools/timeline.py "$db" > $O/${TAG}_timeline_config$C.txt 2>&1 || true
   python3 tools/kernel_audit.py "$db" > $O/${TAG}_kernel_audit_config$C.txt 2>&1 || true
   head -12 $O/${TAG}_timeline_config$C.txt
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetch$C \
-    -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
     > $O/${TAG}_fetch$C.log 2>&1 || { tail -20 $O/${TAG}_fetch$C.log; exit 1; }
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_write$C \
-    -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py --config $C --steps 3 --warmup 1 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
     > $O/${TAG}_write$C.log 2>&1 || { tail -20 $O/${TAG}_write$C.log; exit 1; }
   CB=$([ $C = 2 ] && echo 1.342e9 || echo 5.29e9)
   python3 tools/pmc_traffic.py $O/${TAG}_fetch$C $O/${TAG}_write$C --steps 4 --compulsory $CB \
@@ -59,16 +59,16 @@ done
 if has runet; then
 # config 5 (RDCNet, --runet): kernel stats of its step
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_profrunet \
-  -- python3 bench.py --runet --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing \
+  -- python3 bench.py --runet --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
   > $O/${TAG}_profrunet.log 2>&1 || { tail -30 $O/${TAG}_profrunet.log; exit 1; }
 f=$(find $O/${TAG}_profrunet -name '*kernel_stats.csv' | head -1); cp "$f" $O/${TAG}_kernel_stats_runet.csv
 find $O/${TAG}_profrunet -name '*.csv' -size +20M -delete 2>/dev/null
 # its HBM traffic (FETCH_SIZE / WRITE_SIZE, one pass each; 3 steps profiled)
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/${TAG}_fetchrunet \
-  -- python3 bench.py --runet --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+  -- python3 bench.py --runet --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
   > $O/${TAG}_fetchrunet.log 2>&1 || { tail -20 $O/${TAG}_fetchrunet.log; exit 1; }
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${TAG}_writerunet \
-  -- python3 bench.py --runet --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing \
+  -- python3 bench.py --runet --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
   > $O/${TAG}_writerunet.log 2>&1 || { tail -20 $O/${TAG}_writerunet.log; exit 1; }
 python3 tools/pmc_traffic.py $O/${TAG}_fetchrunet $O/${TAG}_writerunet --steps 3 \
   --out $O/${TAG}_traffic_runet.json > $O/${TAG}_traffic_runet.txt 2>&1 || true

@@ -20,7 +20,7 @@ for P in "$P1" "$P2"; do
   for c in $P; do grep -qx "$c" $O/${TAG}_sq_names.txt || { echo "missing counter $c"; ok=0; }; done
   [ $ok = 1 ] || continue
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/${TAG}_p$i \
-    -- python3 bench.py $BARGS --no-cpu-baseline --no-kernel-timing \
+    -- python3 bench.py $BARGS --no-cpu-baseline --no-kernel-timing --idle-steps 0 \
     > $O/${TAG}_p$i.log 2>&1 || { tail -20 $O/${TAG}_p$i.log; exit 1; }
 done
 python3 tools/pmc_summary.py $O/${TAG}_p1 $O/${TAG}_p2 --top 30 > $O/${TAG}_summary.txt 2>&1
