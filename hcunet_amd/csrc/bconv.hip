@@ -237,7 +237,10 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
   if (a.phy < 1) a.phy = 1;
   if (a.phz < 1) a.phz = 1;
   const int T = a.KX * a.KY * a.KZ;
-  const int Nlog = a.Cout * a.nph;
+  if (a.nph == 1 || a.cph < a.Cout) a.cph = 0;
+  const int CPH = a.cph > 0 ? a.cph : a.Cout;
+  if (a.cph > a.OCs) return fail(4, "bconv: padded phase columns exceed the stored channels");
+  const int Nlog = CPH * a.nph;
   const int nb16 = cdiv(Nlog, 16);
   const int ntz = cdiv(a.OZ, 16);
   a.TZ = cdiv(a.OZ, ntz);
@@ -267,7 +270,7 @@ int plan_bconv(GConvArgs &a, int target_blocks) {
     if (NSUB == 2 && nb16 < 2) continue;
     // (phases folded into N: a lane's 4 columns share a phase; bf16 stores 8
     // channels per 16 bytes of the packed weights)
-    if (a.nph > 1 && (a.Cout % (a.bes == 2 ? 8 : 4))) continue;
+    if (a.nph > 1 && (CPH % (a.bes == 2 ? 8 : 4))) continue;
     const int NT = NSUB * 16;
     const int CoutW = round_up(Nlog, NT);
     const int nN = CoutW / NT;

@@ -230,19 +230,21 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     toffs[e] = off * CKP + ((e & 3) % CV) * VEC;
   }
   // first stored channel of the block (ConvTranspose3d phases folded into N:
-  // column n0 + j is channel (n0 + j) % Cout of phase (n0 + j) / Cout)
-  const int co0 = a.nph > 1 ? n0 - (n0 / a.Cout) * a.Cout : n0;
+  // column n0 + j is channel (n0 + j) % CPH of phase (n0 + j) / CPH, CPH the
+  // columns per phase: Cout, or Cout padded to the store width (GConvArgs::cph))
+  const int CPH = a.cph > 0 ? a.cph : a.Cout;
+  const int co0 = a.nph > 1 ? n0 - (n0 / CPH) * CPH : n0;
   // the 4 stored columns of lane group g in column subtile n: their first
   // channel (-1: past the stored channels) and the output offset of their
-  // phase (Cout % 4 == 0, so the 4 share it; a block may span phases)
+  // phase (CPH % 4 == 0, so the 4 share it; a block may span phases)
   int cn[NSUB], qo[NSUB];
 #pragma unroll
   for (int n = 0; n < NSUB; ++n) {
     const int gcl = n0 + n * 16 + g * 4;
     if (a.nph > 1) {
-      const int ph = gcl / a.Cout;
+      const int ph = gcl / CPH;
       const int qz = ph % a.phz, qy = (ph / a.phz) % a.phy, qx = ph / (a.phz * a.phy);
-      cn[n] = ph < a.nph ? gcl - ph * a.Cout : -1;
+      cn[n] = ph < a.nph ? gcl - ph * CPH : -1;
       qo[n] = ((qx * a.SY + qy) * a.SZ + qz) * a.OCs;
     } else {
       cn[n] = gcl < a.OCs ? gcl : -1;
@@ -465,7 +467,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   };
   auto load_coefs = [&]() {
     for (int j = tid; j < NT; j += 256) {
-      const int c = a.nph > 1 ? (n0 + j) % a.Cout : n0 + j;
+      const int c = a.nph > 1 ? (n0 + j) % CPH : n0 + j;
       coefL[j] = (!split && a.bias && c < a.Cout) ? a.bias[c] : 0.f;
       const bool bn = BNB && !split && c < a.OCs;
       coefL[NT + j] = bn ? a.bn_scale[c] : 0.f;

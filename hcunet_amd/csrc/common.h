@@ -257,6 +257,11 @@ struct GConvArgs {
   // (channels-last activations, packed weights); partial stays fp32.
   int use_bconv;
   int bes;   // bconv element bytes: 2 (bf16 activations) or 4 (fp32); 0 = 2
+  // bconv with ConvTranspose3d phases folded into N: columns per phase (0 =
+  // Cout).  Cout not a multiple of the 4 (fp32) / 8 (bf16) columns a lane's
+  // store and a packed weight vector span: cph = Cout rounded up, the padded
+  // columns have zero weights and zero bias (RDCNet's 5-channel output).
+  int cph;
 };
 
 // Forward BatchNorm statistics rows (stats, [rows][CoutW] of float4): per
@@ -308,6 +313,7 @@ inline int plan_conv_fp32(GConvArgs &a, int target_blocks) {
       return 0;
     }
   }
+  a.cph = 0;   // (bconv only)
   return plan_conv_any(a, target_blocks);
 }
 int launch_bconv(const GConvArgs &a, hipStream_t s);
@@ -616,7 +622,7 @@ struct PrepJob {
   int64_t dst;      // float offset of the prepared buffer in the destination workspace
   WPack pk;
   // CONV_FWD / CONV_DGRAD: Cout, Cin_g, groups, fold_mod, T, rows (ECs|OCs), cols (CoutW|EW), E
-  // CONVT_FUSED: Cin, Cout, KX, KY, KZ, sx, sy, sz, ICs, CoutW
+  // CONVT_FUSED: Cin, Cout, KX, KY, KZ, sx, sy, sz, ICs, CoutW, columns per phase (0: Cout)
   // CONVT_PHASE: Cin, Cout, KX, KY, KZ, sx, sy, sz, px, py, pz, Jx, Jy, Jz, ICs, CoutW
   // CONVT_DGRAD: Cin, Cout, T, UCs, CinW
   int p[16];

@@ -78,8 +78,10 @@ __device__ __forceinline__ float prep_eval(const PrepJob &jb, const float *w, in
       const int Cin = p[0], Cout = p[1], KX = p[2], KY = p[3], KZ = p[4];
       const int sx = p[5], sy = p[6], sz = p[7];
       const int Jx = KX / sx, Jy = KY / sy, Jz = KZ / sz;
-      if (a >= Cin || b >= sx * sy * sz * Cout) return 0.f;
-      const int ph = b / Cout, co = b % Cout;
+      const int cph = p[10] > 0 ? p[10] : Cout;   // columns per phase (GConvArgs::cph)
+      if (a >= Cin || b >= sx * sy * sz * cph) return 0.f;
+      const int ph = b / cph, co = b % cph;
+      if (co >= Cout) return 0.f;
       const int qz = ph % sz, qy = (ph / sz) % sy, qx = ph / (sz * sy);
       const int tz = t % Jz, ty = (t / Jz) % Jy, tx = t / (Jz * Jy);
       const int kx = qx + sx * (Jx - 1 - tx), ky = qy + sy * (Jy - 1 - ty), kz = qz + sz * (Jz - 1 - tz);

@@ -128,6 +128,14 @@ struct ConvTLayer {
   // decoders with kernel % stride == 0 and Cout % 4 == 0
   WGradArgs wgp{};
   bool wg_phase = false;
+  // layer chains, bf16, no BatchNorm+ReLU applied to the input: the weight
+  // gradient as the Conv3d weight gradient of the input-gradient convolution
+  // (rows (tap, co) over the strided dU halo, columns ci over x; finalize
+  // mode 0 with Cout = Cin, Cin_g = Cout -- the [Cin][Cout][K] layout of a
+  // ConvTranspose3d weight is a Conv3d weight's [Cout][Cin][K]): every tap in
+  // one block, instead of a (tap, co)-column GEMM with one 16-row subtile
+  WGradArgs wgs{};
+  bool wg_swap = false;
   size_t u_off = 0;
   size_t wf_off = 0, wd_off = 0;   // prepared weights in `saved` (fused fwd, dgrad)
   std::vector<size_t> wph_off;     // per-phase fwd weights when not fused
@@ -380,6 +388,10 @@ int setup_convt(ConvTLayer &u, const Dims &cur, int o, const int K[3], const int
     a.dx = a.dy = a.dz = 1;
     a.px = Jx - 1; a.py = Jy - 1; a.pz = Jz - 1;
     a.nph = nph; a.phx = u.S[0]; a.phy = u.S[1]; a.phz = u.S[2];
+    // columns per phase padded to the 8 (bf16) / 4 (fp32) a packed vector and
+    // a lane's store span (zero weights and bias; RDCNet's 5 output channels)
+    const int cv = bf ? 8 : 4;
+    if (o % cv) a.cph = round_up(o, cv);
     if (bf) {
       if (int e = plan_bconv(a, kTargetBlocks)) return e;
       u.fwdf = a;
@@ -816,9 +828,9 @@ int build_plan(hcu_unet_plan &p) {
     conv_jobs(p.uc1[j]);
     conv_jobs(p.uc2[j]);
     if (u.fused) {
-      const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
-                          u.fwdf.ICs, u.fwdf.CoutW};
-      add_job(PREP_CONVT_FUSED, prep_elems(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 10, u.wf_off);
+      const int pf[11] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
+                          u.fwdf.ICs, u.fwdf.CoutW, u.fwdf.cph};
+      add_job(PREP_CONVT_FUSED, prep_elems(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 11, u.wf_off);
     } else {
       u.wph_off.assign(u.phases.size(), 0);
       for (size_t ph = 0; ph < u.phases.size(); ++ph) {
@@ -1943,9 +1955,9 @@ int hcu_conv_fwd_cl(const hcu_conv_desc *d, const float *x, const float *w, cons
   if (u.fused) {
     GConvArgs a = u.fwdf;
     if (a.use_bconv) {
-      const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2], a.ICs,
-                          a.CoutW};
-      if (int e = prep_one(PREP_CONVT_FUSED, a, pf, 10, w, wprep, s)) return e;
+      const int pf[11] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2], a.ICs,
+                          a.CoutW, a.cph};
+      if (int e = prep_one(PREP_CONVT_FUSED, a, pf, 11, w, wprep, s)) return e;
     } else if (int e = launch_prep_convt_fused(w, wprep, u.Cin, u.Cout, u.K[0], u.K[1], u.K[2],
                                                u.S[0], u.S[1], u.S[2], a.ICs, a.CoutW,
                                                wpack_of(a), s)) {
@@ -2252,6 +2264,31 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
         p.max_part = std::max(p.max_part, wgrad_partial_floats(w));
         p.max_part = std::max(p.max_part, (size_t)chansum_rows(u.out.vox(), u.out.Cs) * u.out.Cs);
       }
+      u.wg_swap = false;
+      if (bf && !prev_bn && !getenv("HCU_CONVT_NOSWAP")) {
+        // dW[ci][co][k] = sum_o x[o][ci] dU[o*S + k - pad][co]
+        WGradArgs v{};
+        v.B = p.B;
+        v.AX = u.out.X; v.AY = u.out.Y; v.AZ = u.out.Z; v.ACs = u.out.Cs;   // dU (cropped)
+        v.GX = u.in.X; v.GY = u.in.Y; v.GZ = u.in.Z; v.GCs = u.in.Cs;        // x
+        v.PX = u.in.X; v.PY = u.in.Y; v.PZ = u.in.Z;
+        v.KX = u.K[0]; v.KY = u.K[1]; v.KZ = u.K[2];
+        v.asx = u.S[0]; v.asy = u.S[1]; v.asz = u.S[2];
+        v.adx = v.ady = v.adz = 1;
+        v.apx = s.pad[0]; v.apy = s.pad[1]; v.apz = s.pad[2];
+        v.gsx = v.gsy = v.gsz = 1;
+        v.gdx = v.gdy = v.gdz = 1;
+        v.taps_rows = 1;
+        v.bias_row = 0;
+        v.flops = 2.0 * p.B * u.in.X * u.in.Y * u.in.Z * (double)u.T * u.Cin * u.Cout;
+        if (plan_bwgrad(v, kTargetBlocks) == 0) {
+          u.wgs = v;
+          u.wg_swap = true;
+          p.max_part = std::max(p.max_part, wgrad_partial_floats(v));
+        } else {
+          set_error("");
+        }
+      }
       u.u_off = saved.take_floats(u.out.floats());
       p.max_act = std::max(p.max_act, u.out.floats());
       cur = u.out;
@@ -2294,9 +2331,9 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
     } else if (o.kind == HCU_CHAIN_CONVT) {
       ConvTLayer &u = o.ct;
       if (u.fused) {
-        const int pf[10] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
-                            u.fwdf.ICs, u.fwdf.CoutW};
-        add_job(PREP_CONVT_FUSED, prep_elems(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 10, u.wf_off);
+        const int pf[11] = {u.Cin, u.Cout, u.K[0], u.K[1], u.K[2], u.S[0], u.S[1], u.S[2],
+                            u.fwdf.ICs, u.fwdf.CoutW, u.fwdf.cph};
+        add_job(PREP_CONVT_FUSED, prep_elems(u.fwdf), u.w_off, wpack_of(u.fwdf), pf, 11, u.wf_off);
       } else {
         u.wph_off.assign(u.phases.size(), 0);
         for (size_t ph = 0; ph < u.phases.size(); ++ph) {
@@ -2571,7 +2608,29 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
         fb.accumulate = accumulate;
         if (int e = c.pend_wgf(fb)) return e;
       }
-      {
+      if (u.wg_swap && !a.sc) {
+        WGradArgs w = u.wgs;
+        w.A = dU;
+        w.a_scale = w.a_shift = nullptr;
+        w.G = a.x;
+        if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
+        if (int e = launch_wgrad(w, s)) return e;
+        WGradFinalize f{};
+        f.partial = w.partial;
+        f.dw = c.G + u.w_off;
+        f.KB = w.KB;
+        f.Mtot = w.Mtot;
+        f.Ntot = w.Ntot;
+        f.T = u.T;
+        f.mode = 0;
+        f.Cout = u.Cin;
+        f.Cin_g = u.Cout;
+        f.groups = 1;
+        f.fold_mod = u.Cout;
+        f.ACs = w.ACs;
+        f.accumulate = accumulate;
+        if (int e = c.pend_wgf(f)) return e;
+      } else {
         WGradArgs w = u.wg;
         w.A = a.x;
         w.a_scale = a.sc;

@@ -21,8 +21,8 @@ hcu_sum_parts).  StackedDilation's dilated
 5^3 convolutions whose halo does not fit a workgroup run on their dilation
 sub-lattices (space-to-batch, hcunet_amd/csrc/layout.hip).  Under
 torch.autocast('cuda', torch.bfloat16) (or compute_dtype = torch.bfloat16)
-the chains run on the bf16 path; RDCNet's last ConvTranspose3d (5 output
-channels: no bf16 phase-folded tiling) stays fp32.
+the chains run on the bf16 path, RDCNet's last ConvTranspose3d included
+(its 5 output channels padded to 8 columns per stride phase).
 """
 import ctypes
 import glob
@@ -545,8 +545,16 @@ class RDCNet(nn.Module):
             y, yc = resid_add(mix(cl_cat([d(hi, tr, bf16) for d, hi in zip(dil, h)]), tr, bf16), y)
             if trace is not None:
                 trace.append(y.detach().clone())
+        if bf16:
+            # autocast runs the ConvTranspose3d in bf16 too (r_unet.py:227):
+            # out_conv's output stays channels-last bf16 and the phase-folded
+            # ConvTranspose3d reads it directly (its 5 output channels padded
+            # to 8 columns per stride phase, GConvArgs::cph)
+            y = _chain(self, self, 'out_cl2', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],
+                       in_cl=True, out_cl=True)(yc, tr, True)
+            return _chain(self, self, 'convt_cl', self.transposed_conv.in_channels,
+                          [('convt', self.transposed_conv)], in_cl=True)(y, tr, True)
         y = _chain(self, self, 'out_cl', self.out_conv.in_channels, [('conv', self.out_conv, None, False)],
                    in_cl=True)(yc, tr, bf16)
-        # 5 output channels: no bf16 phase-folded ConvTranspose3d tiling; fp32
         return _chain(self, self, 'convt', self.transposed_conv.in_channels,
                       [('convt', self.transposed_conv)])(y, tr, False)

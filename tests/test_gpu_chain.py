@@ -168,3 +168,48 @@ def test_channels_last_boundaries_and_parts(bf16):
             [('grad%d' % i, u, v) for i, (u, v) in enumerate(zip(g0, g1))]:
         err = (u.float() - v.float()).abs().max().item()
         assert err <= tol * max(u.abs().max().item(), 1e-6), (name, err, u.abs().max().item())
+
+
+@pytest.mark.parametrize('in_cl,swap', [(False, True), (True, True), (True, False)])
+def test_convt_chain_bf16_padded_phase_columns(in_cl, swap, monkeypatch):
+    """RDCNet's ConvTranspose3d (10 -> 5, k4, s2, p1; r_unet.py:216) on the
+    bf16 path, where its 5 output channels are padded to 8 columns per stride
+    phase (GConvArgs::cph: zero weights and bias in the padded columns), and
+    its weight gradient taken as the Conv3d weight gradient of the
+    input-gradient convolution (swap; HCU_CONVT_NOSWAP=1: the (tap, co)
+    column form), against fp64 torch on the same bf16-representable input,
+    weights and upstream gradient: output and input gradient to bf16 storage
+    precision, weight / bias gradients (fp32 accumulation of exact products)
+    to 2e-3."""
+    from hcunet_amd.chain import cl_channels
+    if not swap:
+        monkeypatch.setenv('HCU_CONVT_NOSWAP', '1')
+    torch.manual_seed(6)
+    ct = nn.ConvTranspose3d(10, 5, 4, stride=2, padding=1)
+    with torch.no_grad():
+        ct.weight.copy_(ct.weight.bfloat16().float())
+    x = torch.randn((1, 10, 20, 18, 6), generator=torch.Generator().manual_seed(7)).bfloat16().float()
+    ref = copy.deepcopy(ct).double()
+    xr = x.double().requires_grad_(True)
+    y = ref(xr)
+    g = torch.randn(y.shape, generator=torch.Generator().manual_seed(8)).bfloat16().double()
+    (y * g).sum().backward()
+    holder = _Holder(copy.deepcopy(ct)).cuda()
+    ch = Chain(FlatParams(holder), 10, [('convt', holder.m[0])], in_cl=in_cl)
+    if in_cl:
+        xg = _to_cl(x.cuda(), cl_channels(10, True), torch.bfloat16).requires_grad_(True)
+    else:
+        xg = x.cuda().requires_grad_(True)
+    out = ch(xg, True, True)
+    assert out.shape == y.shape and out.dtype == torch.float32
+    (out * g.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    dx = xg.grad[..., :10].float().permute(0, 4, 1, 2, 3) if in_cl else xg.grad
+    if in_cl:
+        assert not xg.grad[..., 10:].any()
+    m = holder.m[0]
+    for name, got, want, tol in [('out', out.detach(), y.detach(), 1e-2), ('dx', dx, xr.grad, 1e-2),
+                                 ('dW', m.weight.grad, ref.weight.grad, 2e-3),
+                                 ('db', m.bias.grad, ref.bias.grad, 2e-3)]:
+        err = (got.cpu().double() - want).abs().max().item()
+        assert err <= tol * want.abs().max().item(), (name, err, want.abs().max().item())
