@@ -285,6 +285,9 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
 
   // ---- one partial slab per block: each wave writes its own rows
   const size_t slab = (size_t)blockIdx.x * a.Mtot;
+  // taps_rows slab rows (tap, real channel) and columns (real channels):
+  // WGradArgs::ACr / GCr, the padding slots of the channel strides not stored
+  const int ACR = a.ACr > 0 ? a.ACr : a.ACs, GCR = a.GCr > 0 ? a.GCr : a.GCs;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
 #pragma unroll
@@ -294,7 +297,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
       if (lr < rows_blk) {
         if (a.taps_rows) {
           const int ta = t0 + lr / CKA, ci = ci0 + lr % CKA;
-          if (ta < T && ci < a.ACs) grow = ta * a.ACs + ci;
+          if (ta < T && ci < ACR) grow = ta * ACR + ci;
         } else if (ci0 + lr < a.ACs) {
           grow = ci0 + lr;
         }
@@ -306,7 +309,7 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
         int gcol = -1;
         if (lc < cols_blk) {
           if (a.taps_rows) {
-            if (co0 + lc < a.GCs) gcol = co0 + lc;
+            if (co0 + lc < GCR) gcol = co0 + lc;
           } else {
             const int tg = t0 + lc / CKG, o = co0 + lc % CKG;
             if (tg < T && o < a.GCs) gcol = tg * a.GCs + o;
@@ -320,8 +323,8 @@ __global__ void __launch_bounds__(256) bwgrad_kernel(const WGradArgs a) {
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
       const int lc = n * 16 + (lane & 15);
-      if (lc < CKG && co0 + lc < a.GCs)
-        a.partial[(slab + (size_t)T * a.ACs) * a.Ntot + co0 + lc] = accb[n][0];
+      if (lc < CKG && co0 + lc < GCR)
+        a.partial[(slab + (size_t)T * ACR) * a.Ntot + co0 + lc] = accb[n][0];
     }
   }
 }
@@ -659,6 +662,9 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
   }
 #endif
   const size_t slab = (size_t)blockIdx.x * a.Mtot;
+  // taps_rows slab rows (tap, real channel) and columns (real channels):
+  // WGradArgs::ACr / GCr, the padding slots of the channel strides not stored
+  const int ACR = a.ACr > 0 ? a.ACr : a.ACs, GCR = a.GCr > 0 ? a.GCr : a.GCs;
 #pragma unroll
   for (int m = 0; m < MSW; ++m) {
 #pragma unroll
@@ -668,7 +674,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
       if (lr < rows_blk) {
         if (a.taps_rows) {
           const int ta = t0 + lr / CKA, ci = ci0 + lr % CKA;
-          if (ta < T && ci < a.ACs) grow = ta * a.ACs + ci;
+          if (ta < T && ci < ACR) grow = ta * ACR + ci;
         } else if (ci0 + lr < a.ACs) {
           grow = ci0 + lr;
         }
@@ -680,7 +686,7 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
         int gcol = -1;
         if (lc < cols_blk) {
           if (a.taps_rows) {
-            if (co0 + lc < a.GCs) gcol = co0 + lc;
+            if (co0 + lc < GCR) gcol = co0 + lc;
           } else {
             const int tg = t0 + lc / CKG, o = co0 + lc % CKG;
             if (tg < T && o < a.GCs) gcol = tg * a.GCs + o;
@@ -694,8 +700,8 @@ __global__ void __launch_bounds__(256) bwgrad_pipe_kernel(const WGradArgs a) {
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
       const int lc = n * 16 + (lane & 15);
-      if (lc < CKG && co0 + lc < a.GCs)
-        a.partial[(slab + (size_t)T * a.ACs) * a.Ntot + co0 + lc] = accb[n][0];
+      if (lc < CKG && co0 + lc < GCR)
+        a.partial[(slab + (size_t)T * ACR) * a.Ntot + co0 + lc] = accb[n][0];
     }
   }
 }
@@ -795,8 +801,11 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
   a.nco = a.GCs / a.CKG;
   a.mchunks = a.taps_rows ? a.ntc * a.nci : a.nci;
   a.nchunks = a.taps_rows ? a.nco : a.ntc * a.nco;
-  a.Mtot = a.taps_rows ? T * a.ACs + (a.bias_row ? 1 : 0) : a.ACs;
-  a.Ntot = a.taps_rows ? a.GCs : T * a.GCs;
+  if (!a.taps_rows || a.ACr >= a.ACs) a.ACr = 0;
+  if (!a.taps_rows || a.GCr >= a.GCs) a.GCr = 0;
+  const int ACR = a.ACr > 0 ? a.ACr : a.ACs, GCR = a.GCr > 0 ? a.GCr : a.GCs;
+  a.Mtot = a.taps_rows ? T * ACR + (a.bias_row ? 1 : 0) : a.ACs;
+  a.Ntot = a.taps_rows ? GCR : T * a.GCs;
   // voxel tile: TX*TY = 32 (or 64 when the halo fits), TZ = the whole Z (<= 16)
   // (TZ <= 8 for every layer -- half the image, two resident blocks, twice
   // the slabs -- measured 7.25 vs 6.63 ms per config-3 step)
@@ -859,7 +868,9 @@ static int plan_bwgrad_cka(WGradArgs &a, int cka_cap, bool alltaps) {
   // reads little) takes half the Z extent per tile: two resident blocks
   // Config 3 (interleaved A/B, 2 runs): slabs <= 64 KB (d0.c2, u3.c2) 6.50 vs
   // 6.62 ms/step without; <= 160 KB 6.56; <= 640 KB 6.96.
-  if (!alltaps && lds > 80 * 1024 && (long)a.Mtot * a.Ntot * 4 <= 64 * 1024 && a.PZ > 8) {
+  // (the slab size with the padding slots: the measured rule predates ACr / GCr)
+  const long slab_pad = a.taps_rows ? ((long)T * a.ACs + (a.bias_row ? 1 : 0)) * a.GCs : (long)a.Mtot * a.Ntot;
+  if (!alltaps && lds > 80 * 1024 && slab_pad * 4 <= 64 * 1024 && a.PZ > 8) {
     ntz = cdiv(a.PZ, 8);
     a.TZ = cdiv(a.PZ, ntz);
     const int TZh = a.TZ;

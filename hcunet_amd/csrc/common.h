@@ -388,7 +388,14 @@ struct WGradArgs {
   // stride phases are extra output columns and the bias row sums dU per
   // (q, co) -- no separate chansum.  nph <= 1: plain Conv3d form.
   int nph, phx, phy, phz, GCout;
+  // bwgrad, taps_rows: real input / output channels (0: ACs / GCs).  The slab
+  // rows are (tap, channel < ACr) and its columns channels < GCr, so the
+  // padding slots of a channels-last stride (RDCNet: 10 channels in 16) are
+  // neither written nor summed; wgrad_finalize then takes ACs = ACr.
+  int ACr, GCr;
 };
+// the row stride per tap of a weight-gradient slab (WGradFinalize::ACs)
+inline int wgrad_slab_acs(const WGradArgs &w) { return w.use_bw && w.ACr > 0 ? w.ACr : w.ACs; }
 int plan_bwgrad(WGradArgs &a, int target_blocks);
 int launch_bwgrad(const WGradArgs &a, hipStream_t s);
 int plan_wgrad(WGradArgs &a, int target_blocks);

@@ -195,6 +195,17 @@ WGradArgs wgrad_conv(const Dims &in, const Dims &out, const int K[3], const int 
   return w;
 }
 
+// bf16 Conv3d weight gradients store slab rows of real input channels and
+// columns of real output channels only (WGradArgs::ACr / GCr): RDCNet's
+// 10-channel tensors sit in 16-slot strides.  Inputs made of channel parts
+// keep every packed slot (finalize maps torch channels to packed slots).
+void compact_slab(WGradArgs &w, const ConvLayer &L, bool bf) {
+  w.ACr = w.GCr = 0;
+  if (!bf) return;
+  if (L.part_c == 0 && L.groups == 1) w.ACr = L.E;
+  w.GCr = L.Cout;
+}
+
 // An input made of channel parts (Dims::part_c): every packed channel e of
 // the input stride is a GEMM row (the padding ones get zero weights), and
 // e maps to torch channel (e / part_cs) * part_c + e % part_cs.
@@ -257,6 +268,7 @@ int setup_conv_general(ConvLayer &L, const Dims &in, int Cout, int groups, int f
     WGradArgs w = wgrad_conv(in, L.out, L.K, L.D);
     w.asx = L.S[0]; w.asy = L.S[1]; w.asz = L.S[2];
     w.apx = L.P[0]; w.apy = L.P[1]; w.apz = L.P[2];
+    compact_slab(w, L, bf);
     const int ew = bf ? plan_bwgrad(w, kTargetBlocks) : plan_wgrad(w, kTargetBlocks);
     const bool dil = L.D[0] > 1 || L.D[1] > 1 || L.D[2] > 1;
     if (!ef && !ed && !ew) {
@@ -300,6 +312,7 @@ int setup_conv_general(ConvLayer &L, const Dims &in, int Cout, int groups, int f
     if (int e = plan_c(L.dgrad)) return e;
     L.wg = wgrad_conv(L.sub_in, L.sub_out, L.K, one);
     L.wg.apx = Pd[0]; L.wg.apy = Pd[1]; L.wg.apz = Pd[2];
+    compact_slab(L.wg, L, bf);
     if (int e = bf ? plan_bwgrad(L.wg, kTargetBlocks) : plan_wgrad(L.wg, kTargetBlocks)) return e;
   }
   L.bn.C = Cout;
@@ -344,6 +357,7 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
   if (int e = bf ? plan_bconv(L.dgrad, kTargetBlocks) : plan_conv_fp32(L.dgrad, kTargetBlocks))
     return e;
   L.wg = wgrad_conv(in, L.out, K, D);
+  compact_slab(L.wg, L, bf);
   if (int e = bf ? plan_bwgrad(L.wg, kTargetBlocks) : plan_wgrad(L.wg, kTargetBlocks)) return e;
   L.bn.C = Cout;
   L.bn.Cs = L.out.Cs;
@@ -1118,7 +1132,7 @@ int conv_wgrad(Ctx &c, const ConvLayer &L, const float *A, const float *asc, con
   f.fold_mod = L.fold_mod;
   f.part_c = L.part_c;
   f.part_cs = L.part_cs;
-  f.ACs = w.ACs;
+  f.ACs = wgrad_slab_acs(w);
   f.accumulate = accumulate;
   if (int e = c.pend_wgf(f)) return e;   // finalized with the next flush (Ctx::slab / end of backward)
   return c.read_done(dy_slot);
@@ -2061,7 +2075,7 @@ int hcu_conv_wgrad_cl(const hcu_conv_desc *d, const float *x, const float *dy, f
   f.KB = w.KB;
   f.Mtot = w.Mtot;
   f.Ntot = w.Ntot;
-  f.ACs = w.ACs;
+  f.ACs = wgrad_slab_acs(w);
   f.GCs = w.GCs;
   if (int e = launch_wgrad_finalize(f, s)) return e;
   if (d->transposed && dbias) {
@@ -2280,6 +2294,8 @@ int build_chain(hcu_unet_plan &p, const hcu_chain_spec &cs) {
         v.gdx = v.gdy = v.gdz = 1;
         v.taps_rows = 1;
         v.bias_row = 0;
+        v.ACr = u.Cout;
+        v.GCr = u.Cin;
         v.flops = 2.0 * p.B * u.in.X * u.in.Y * u.in.Z * (double)u.T * u.Cin * u.Cout;
         if (plan_bwgrad(v, kTargetBlocks) == 0) {
           u.wgs = v;
@@ -2627,7 +2643,7 @@ int enqueue_chain_backward(const hcu_unet_plan &p, const hcu_unet_tensors *t, co
         f.Cin_g = u.Cout;
         f.groups = 1;
         f.fold_mod = u.Cout;
-        f.ACs = w.ACs;
+        f.ACs = wgrad_slab_acs(w);
         f.accumulate = accumulate;
         if (int e = c.pend_wgf(f)) return e;
       } else {

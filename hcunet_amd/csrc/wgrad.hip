@@ -549,6 +549,7 @@ static int plan_wgrad2(WGradArgs &a, int target_blocks) {
 
 int plan_wgrad(WGradArgs &a, int target_blocks) {
   const int T = a.KX * a.KY * a.KZ;
+  a.ACr = a.GCr = 0;   // (bwgrad only)
   if (a.ACs % 4 || a.GCs % 4) return fail(1, "wgrad: channel strides must be multiples of 4");
   if (a.PX <= 0 || a.PY <= 0 || a.PZ <= 0) return fail(2, "wgrad: empty grid");
   const int nss[3] = {4, 2, 1};
