@@ -6,7 +6,7 @@ cd "$(dirname "$0")"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 OUT=${OUT:-hcunet_amd/libhcunet.so}   # (OUT / BDIR: a variant build for A/B runs)
 BDIR=${BDIR:-build}
-SRC="hcunet_amd/csrc/timing.cpp hcunet_amd/csrc/gconv.hip hcunet_amd/csrc/conv2.hip hcunet_amd/csrc/conv8.hip hcunet_amd/csrc/wgrad.hip hcunet_amd/csrc/wgrad8.hip hcunet_amd/csrc/wgrad3.hip hcunet_amd/csrc/pointwise.hip hcunet_amd/csrc/loss_adam.hip hcunet_amd/csrc/loss_ext.hip hcunet_amd/csrc/prep_all.hip hcunet_amd/csrc/bconv.hip hcunet_amd/csrc/bconv_f32.hip hcunet_amd/csrc/bconv_f32_cv1.hip hcunet_amd/csrc/bconv_f32_cv2.hip hcunet_amd/csrc/bconv_f32_cv4.hip hcunet_amd/csrc/bconv_bf16_cv1.hip hcunet_amd/csrc/bconv_bf16_cv2.hip hcunet_amd/csrc/bconv_bf16_cv4.hip hcunet_amd/csrc/bwgrad.hip hcunet_amd/csrc/segment.hip hcunet_amd/csrc/ingest.hip hcunet_amd/csrc/layout.hip hcunet_amd/csrc/unet.cpp"
+SRC="hcunet_amd/csrc/timing.cpp hcunet_amd/csrc/gconv.hip hcunet_amd/csrc/conv2.hip hcunet_amd/csrc/conv8.hip hcunet_amd/csrc/wgrad.hip hcunet_amd/csrc/wgrad8.hip hcunet_amd/csrc/wgrad3.hip hcunet_amd/csrc/pointwise.hip hcunet_amd/csrc/loss_adam.hip hcunet_amd/csrc/loss_ext.hip hcunet_amd/csrc/prep_all.hip hcunet_amd/csrc/bconv.hip hcunet_amd/csrc/bconv_f32.hip hcunet_amd/csrc/bconv_f32_cv1.hip hcunet_amd/csrc/bconv_f32_cv2.hip hcunet_amd/csrc/bconv_f32_cv4.hip hcunet_amd/csrc/bconv_bf16_cv1.hip hcunet_amd/csrc/bconv_bf16_cv2.hip hcunet_amd/csrc/bconv_bf16_cv4.hip hcunet_amd/csrc/bwgrad.hip hcunet_amd/csrc/segment.hip hcunet_amd/csrc/ingest.hip hcunet_amd/csrc/layout.hip hcunet_amd/csrc/pwconv.hip hcunet_amd/csrc/unet.cpp"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude $*"
 mkdir -p "$BDIR"
 objs=()

@@ -394,6 +394,20 @@ struct WGradArgs {
   // neither written nor summed; wgrad_finalize then takes ACs = ACr.
   int ACr, GCr;
 };
+// 1x1x1 Conv3d forward / input gradient on bf16 channels-last tensors
+// without BatchNorm (pwconv.hip): RDCNet's mixing convolutions.  Weights in
+// the PyTorch layout [Cout][Cin]; part_c / part_cs: ConvLayer's channel parts.
+//   dgrad 0: in [nvox][ICs] -> out [nvox][OCs] (+ bias)
+//   dgrad 1: in = dy [nvox][ICs = the forward's OCs] -> out = dx [nvox][OCs = the forward's ICs]
+struct PwArgs {
+  const uint16_t *in;
+  const float *w, *bias;
+  uint16_t *out;
+  long nvox;
+  int ICs, OCs, Cin, Cout, part_c, part_cs, dgrad;
+};
+bool pw_supported(int ICs, int OCs, int Cout, bool dgrad);
+int launch_pw(const PwArgs &a, hipStream_t s);
 // the row stride per tap of a weight-gradient slab (WGradFinalize::ACs)
 inline int wgrad_slab_acs(const WGradArgs &w) { return w.use_bw && w.ACr > 0 ? w.ACr : w.ACs; }
 int plan_bwgrad(WGradArgs &a, int target_blocks);

@@ -101,6 +101,7 @@ struct ConvLayer {
   // wgrad are planned as dilation-1 convolutions on them (padding P/D).
   bool s2b = false;
   int L3[3] = {1, 1, 1};                   // lattice (= D) of the s2b form
+  bool pw = false;                         // bf16 1x1x1, no BatchNorm input: pwconv.hip (forward, dgrad)
   Dims sub_in, sub_out;                    // sub-grid tensors (batch B*D)
   int64_t w_off = 0, b_off = 0;
   Dims in, out;
@@ -215,6 +216,20 @@ void set_parts(ConvLayer &L, const Dims &in) {
   if (in.part_c) L.E = in.Cs;
 }
 
+// A bf16 1x1x1 Conv3d (stride 1, no padding, one group, no cat fold) takes the
+// streaming pointwise kernels for its forward and input gradient when its
+// input carries no BatchNorm+ReLU (checked at launch) and it has none itself
+// (the chain's non-BatchNorm branch).  HCU_PW=0: bconv everywhere (A/B).
+void set_pw(ConvLayer &L, const Dims &in, int cin_total) {
+  static const bool off = getenv("HCU_PW") && getenv("HCU_PW")[0] == '0';
+  L.pw = false;
+  if (off || in.es != 2 || L.groups != 1 || L.fold_mod < cin_total) return;
+  for (int i = 0; i < 3; ++i)
+    if (L.K[i] != 1 || L.S[i] != 1 || L.P[i] != 0) return;
+  L.pw = pw_supported(in.Cs, L.out.Cs, L.Cout, false) &&
+         (!L.has_dgrad || pw_supported(in.Cs, L.out.Cs, L.Cout, true));
+}
+
 // Conv3d with stride / zero padding (nn.Conv3d(..., stride, padding), the
 // r_unet.py layers): out = floor((in + 2P - D(K-1) - 1) / S) + 1.  Forward:
 // o*S + t*D - P; input gradient (stride 1): the full correlation with padding
@@ -318,6 +333,7 @@ int setup_conv_general(ConvLayer &L, const Dims &in, int Cout, int groups, int f
   L.bn.C = Cout;
   L.bn.Cs = L.out.Cs;
   L.bn.count = (double)L.out.vox();
+  set_pw(L, in, cin_total);
   return 0;
 }
 
@@ -362,6 +378,7 @@ int setup_conv(ConvLayer &L, const Dims &in, int Cout, int groups, int fold_mod,
   L.bn.C = Cout;
   L.bn.Cs = L.out.Cs;
   L.bn.count = (double)L.out.vox();
+  set_pw(L, in, cin_total);
   return 0;
 }
 
@@ -1148,6 +1165,21 @@ int conv_backward(Ctx &c, const ConvLayer &L, const float *A, const float *asc,
     if (int e = conv_wgrad(c, L, A, asc, ash, dy, dy_slot, accumulate)) return e;
   if (!dA) return 0;
   tag(L.name, "dgrad");
+  if (L.pw && !bnl && !colsum) {   // (the chains' non-BatchNorm 1x1x1 convolutions)
+    PwArgs w{};
+    w.in = reinterpret_cast<const uint16_t *>(dy);
+    w.w = c.P + L.w_off;
+    w.out = reinterpret_cast<uint16_t *>(dA);
+    w.nvox = L.out.vox();
+    w.ICs = L.out.Cs;
+    w.OCs = L.in.Cs;
+    w.Cin = L.Cin_g;
+    w.Cout = L.Cout;
+    w.part_c = L.part_c;
+    w.part_cs = L.part_cs;
+    w.dgrad = 1;
+    return launch_pw(w, c.s);
+  }
   GConvArgs a = L.dgrad;
   a.in = dy;
   a.w = c.fptr(c.wimg(), L.wd_off);
@@ -2460,6 +2492,21 @@ int enqueue_chain_forward(const hcu_unet_plan &p, const hcu_unet_tensors *t, int
         if (int e = launch_b2s(ys, y, p.B, L.out.X, L.out.Y, L.out.Z, L.out.Cs, es, L.L3, so, s)) return e;
       } else if (o.bn_relu) {
         if (int e = conv_forward(c, L, a.x, a.sc, a.sh, training)) return e;
+      } else if (L.pw && !a.sc) {
+        tag(L.name, "fwd");
+        PwArgs w{};
+        w.in = reinterpret_cast<const uint16_t *>(a.x);
+        w.w = c.P + L.w_off;
+        w.bias = L.b_off >= 0 ? c.P + L.b_off : nullptr;
+        w.out = reinterpret_cast<uint16_t *>(y);
+        w.nvox = L.out.vox();
+        w.ICs = L.in.Cs;
+        w.OCs = L.out.Cs;
+        w.Cin = L.Cin_g;
+        w.Cout = L.Cout;
+        w.part_c = L.part_c;
+        w.part_cs = L.part_cs;
+        if (int e = launch_pw(w, s)) return e;
       } else {
         tag(L.name, "fwd");
         GConvArgs g = L.fwd;

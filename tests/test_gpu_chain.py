@@ -213,3 +213,55 @@ def test_convt_chain_bf16_padded_phase_columns(in_cl, swap, monkeypatch):
                                  ('db', m.bias.grad, ref.bias.grad, 2e-3)]:
         err = (got.cpu().double() - want).abs().max().item()
         assert err <= tol * want.abs().max().item(), (name, err, want.abs().max().item())
+
+
+@pytest.mark.parametrize('cin,cout,part', [(50, 10, 10), (20, 10, 10), (16, 16, 0)])
+def test_pointwise_conv_chain_bf16(cin, cout, part):
+    """The streaming 1x1x1 kernels (pwconv.hip) of the bf16 chains: RDCNet's
+    mixing convolutions (StackedDilation.out_conv 50 -> 10 and RDCBlock.conv
+    20 -> 10 on channel parts of 10 channels in 16 slots, r_unet.py:354-374)
+    and a plain 16 -> 16 one, channels-last in and out, against fp64 torch on
+    the same bf16-representable input, weights and upstream gradient: output
+    and input gradient to bf16 storage precision, weight / bias gradients to
+    2e-3; every padding slot of the output and of the input gradient 0."""
+    from hcunet_amd.chain import cl_channels
+    torch.manual_seed(11)
+    conv = nn.Conv3d(cin, cout, 1)
+    with torch.no_grad():
+        conv.weight.copy_(conv.weight.bfloat16().float())
+    shape = (1, cin, 24, 20, 6)
+    x = torch.randn(shape, generator=torch.Generator().manual_seed(12)).bfloat16().float()
+    ref = copy.deepcopy(conv).double()
+    xr = x.double().requires_grad_(True)
+    y = ref(xr)
+    g = torch.randn(y.shape, generator=torch.Generator().manual_seed(13)).bfloat16().double()
+    (y * g).sum().backward()
+    holder = _Holder(copy.deepcopy(conv)).cuda()
+    m = holder.m[0]
+    if part:
+        ps = cl_channels(part, True)
+        xin = torch.cat([_to_cl(x[:, i:i + part].cuda(), ps, torch.bfloat16) for i in range(0, cin, part)], -1)
+        ch = Chain(FlatParams(holder), cin, [('conv', m, None, False)], in_cl=True, out_cl=True, in_part=part)
+    else:
+        ps = cl_channels(cin, True)
+        xin = _to_cl(x.cuda(), ps, torch.bfloat16)
+        ch = Chain(FlatParams(holder), cin, [('conv', m, None, False)], in_cl=True, out_cl=True)
+    xin = xin.requires_grad_(True)
+    out = ch(xin, True, True)
+    cs = cl_channels(cout, True)
+    assert out.shape == (1,) + shape[2:] + (cs,) and out.dtype == torch.bfloat16
+    assert not out[..., cout:].any()
+    (out.float() * _to_cl(g.float().cuda(), cs, torch.float32)).sum().backward()
+    torch.cuda.synchronize()
+    got_y = out[..., :cout].float().permute(0, 4, 1, 2, 3)
+    if part:
+        parts = xin.grad.reshape(xin.shape[:-1] + (cin // part, ps))
+        assert not parts[..., part:].any()
+        dx = parts[..., :part].reshape(xin.shape[:-1] + (cin,)).float().permute(0, 4, 1, 2, 3)
+    else:
+        dx = xin.grad[..., :cin].float().permute(0, 4, 1, 2, 3)
+    for name, got, want, tol in [('out', got_y, y.detach(), 1e-2), ('dx', dx, xr.grad, 1e-2),
+                                 ('dW', m.weight.grad, ref.weight.grad, 2e-3),
+                                 ('db', m.bias.grad, ref.bias.grad, 2e-3)]:
+        err = (got.cpu().double() - want).abs().max().item()
+        assert err <= tol * want.abs().max().item(), (name, err, want.abs().max().item())
