@@ -408,6 +408,18 @@ struct PwArgs {
 };
 bool pw_supported(int ICs, int OCs, int Cout, bool dgrad);
 int launch_pw(const PwArgs &a, hipStream_t s);
+// Their weight / bias gradient (pwconv.hip): A = x [nvox][ACs], G = dy
+// [nvox][GCs]; one slab per block in bwgrad's taps_rows layout (T = 1): rows
+// e < ACR, the bias row ACR (bias_row), columns o < GCR, Mtot x Ntot floats.
+struct PwWgArgs {
+  const uint16_t *A, *G;
+  float *partial;
+  long nvox, per_block;
+  int ACs, GCs, ACR, GCR, Mtot, Ntot, bias_row;
+};
+bool pw_wgrad_supported(int ACs, int GCs);
+int pw_wgrad_blocks(long nvox);
+int launch_pw_wgrad(const PwWgArgs &a, int blocks, hipStream_t s);
 // the row stride per tap of a weight-gradient slab (WGradFinalize::ACs)
 inline int wgrad_slab_acs(const WGradArgs &w) { return w.use_bw && w.ACr > 0 ? w.ACr : w.ACs; }
 int plan_bwgrad(WGradArgs &a, int target_blocks);

@@ -121,6 +121,113 @@ __global__ void __launch_bounds__(256) pw_kernel(const PwArgs a) {
   }
 }
 
+// Weight and bias gradient of the same 1x1x1 convolutions, on the VALU:
+//   dW[e][o] = sum_v A[v][e] * G[v][o],   db[o] = sum_v G[v][o]
+// (80 x 16 slots at most: 1.3 KFLOP per voxel, too little to stage for the
+// MFMA's voxel-major K through transposed LDS reads).  A block takes a
+// contiguous voxel range in 64-voxel chunks (the next chunk's 16-byte loads in
+// registers while the current one is summed from LDS); a thread owns 8 input
+// slots x 8 output channels (64 fp32 accumulators from 32 B of LDS per voxel:
+// 4 bytes of LDS per accumulator update was the limit of a 8 x 4 ownership)
+// for one voxel subset; the subsets are summed in a fixed order at the end
+// and the block writes one slab in bwgrad's taps_rows layout (WGradArgs Mtot
+// / Ntot / ACr / GCr, bias row last) for wgrad_finalize.
+constexpr int kPwNV = 64;        // voxels per chunk
+constexpr int kPwLoads = 4;      // 16-byte staging loads per thread and chunk (A + G)
+
+__global__ void __launch_bounds__(256) pw_wgrad_kernel(const PwWgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint4 pw_lds[];
+  const int tid = threadIdx.x;
+  const int E8 = a.ACs / 8, G8 = a.GCs / 8;
+  const int U = E8 * G8 + G8, VS = 256 / U;   // units: (slot octet, channel octet) pairs + bias octets
+  const int sub = tid / U, u = tid - sub * U;
+  const bool active = sub < VS;
+  const bool isb = u >= E8 * G8;
+  const int e8 = isb ? 0 : u / G8, o8 = isb ? u - E8 * G8 : u % G8;
+  float acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  const long v0 = (long)blockIdx.x * a.per_block;
+  const long v1 = v0 + a.per_block < a.nvox ? v0 + a.per_block : a.nvox;
+  uint4 *la = pw_lds;                      // [kPwNV][E8]
+  uint4 *lg = pw_lds + kPwNV * E8;         // [kPwNV][G8]
+  const int nA = kPwNV * E8, nAll = kPwNV * (E8 + G8);
+  uint4 rr[kPwLoads];
+  auto load = [&](long c0) {
+#pragma unroll
+    for (int k = 0; k < kPwLoads; ++k) {
+      const int i = tid + k * 256;
+      uint4 w = make_uint4(0u, 0u, 0u, 0u);
+      if (i < nAll) {
+        const bool isA = i < nA;
+        const int ii = isA ? i : i - nA, per = isA ? E8 : G8;
+        const int v = ii / per, q = ii - v * per;
+        if (c0 + v < v1)
+          w = isA ? *reinterpret_cast<const uint4 *>(a.A + (c0 + v) * a.ACs + q * 8)
+                  : *reinterpret_cast<const uint4 *>(a.G + (c0 + v) * a.GCs + q * 8);
+      }
+      rr[k] = w;
+    }
+  };
+  if (v0 < v1) load(v0);
+  for (long c0 = v0; c0 < v1; c0 += kPwNV) {
+    __syncthreads();   // the previous chunk is consumed
+#pragma unroll
+    for (int k = 0; k < kPwLoads; ++k) {
+      const int i = tid + k * 256;
+      if (i < nAll) pw_lds[i] = rr[k];
+    }
+    __syncthreads();
+    if (c0 + kPwNV < v1) load(c0 + kPwNV);   // lands while this chunk is summed
+    const int nv = v1 - c0 < kPwNV ? (int)(v1 - c0) : kPwNV;
+    if (active) {
+      for (int v = sub; v < nv; v += VS) {
+        float g[8];
+        unpack8(lg[v * G8 + o8], g);
+        if (!isb) {
+          float x[8];
+          unpack8(la[v * E8 + e8], x);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(x[i], g[j], acc[i][j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[0][j] += g[j];
+        }
+      }
+    }
+  }
+  // the voxel subsets' sums in a fixed order, in two halves of 32
+  // accumulators (the reduction area [VS][U][32] fits the LDS of a block)
+  float *red = reinterpret_cast<float *>(pw_lds);
+  float *slab = a.partial + (size_t)blockIdx.x * a.Mtot * a.Ntot;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();
+    if (active)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[((size_t)sub * U + u) * 32 + i * 8 + j] = acc[4 * h + i][j];
+    __syncthreads();
+    for (int w = tid; w < U * 32; w += 256) {
+      const int uu = w >> 5, q = w & 31, i = 4 * h + (q >> 3), j = q & 7;
+      float sum = 0.f;
+      for (int ss = 0; ss < VS; ++ss) sum += red[((size_t)ss * U + uu) * 32 + q];
+      if (uu < E8 * G8) {
+        const int e = (uu / G8) * 8 + i, o = (uu % G8) * 8 + j;
+        if (e < a.ACR && o < a.GCR) slab[(size_t)e * a.Ntot + o] = sum;
+      } else if (i == 0 && a.bias_row) {
+        const int o = (uu - E8 * G8) * 8 + j;
+        if (o < a.GCR) slab[(size_t)a.ACR * a.Ntot + o] = sum;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 bool pw_supported(int ICs, int OCs, int Cout, bool dgrad) {
@@ -128,6 +235,32 @@ bool pw_supported(int ICs, int OCs, int Cout, bool dgrad) {
   // dgrad: K = the gradient's OCs (<= 32), N = ICs output slots (<= 96)
   if (ICs % 8 || OCs % 8 || Cout > OCs) return false;
   return dgrad ? (OCs <= 32 && ICs <= 96) : (ICs <= 128 && OCs <= 32);
+}
+
+bool pw_wgrad_supported(int ACs, int GCs) {
+  if (ACs % 8 || GCs % 8 || ACs > 128 || GCs > 32) return false;
+  const int U = (ACs / 8) * (GCs / 8) + GCs / 8;
+  return U <= 256 && kPwNV * (ACs / 8 + GCs / 8) <= kPwLoads * 256;
+}
+
+int pw_wgrad_blocks(long nvox) {
+  // one resident round: 136 VGPRs leave 3 waves per SIMD = 3 blocks per CU
+  // (1024 blocks ran a second round of 256: 62 vs ~31 us), >= 4 chunks a block
+  const long b = (nvox + 4 * kPwNV - 1) / (4 * kPwNV);
+  return (int)std::max(1L, std::min(b, 768L));
+}
+
+int launch_pw_wgrad(const PwWgArgs &a, int blocks, hipStream_t s) {
+  if (!pw_wgrad_supported(a.ACs, a.GCs)) return fail(4, "pwconv: unsupported weight-gradient channels");
+  const int E8 = a.ACs / 8, G8 = a.GCs / 8;
+  const int U = E8 * G8 + G8, VS = 256 / U;
+  const size_t lds = std::max((size_t)kPwNV * (E8 + G8) * 16, (size_t)VS * U * 32 * 4);
+  const double fl = 2.0 * a.nvox * (double)a.ACR * a.GCR;
+  const double by = 2.0 * a.nvox * (double)(a.ACs + a.GCs);
+  HCU_TIMED(s, "pw_wgrad_kernel", fl, by,
+            HCU_LAUNCH(pw_wgrad_kernel, dim3(blocks), dim3(256), lds, s, a));
+  HCU_CHECK_LAUNCH();
+  return 0;
 }
 
 int launch_pw(const PwArgs &a, hipStream_t s) {

@@ -102,6 +102,7 @@ struct ConvLayer {
   bool s2b = false;
   int L3[3] = {1, 1, 1};                   // lattice (= D) of the s2b form
   bool pw = false;                         // bf16 1x1x1, no BatchNorm input: pwconv.hip (forward, dgrad)
+  bool pw_wg = false;                      // ... and its weight gradient (pw_wgrad_kernel)
   Dims sub_in, sub_out;                    // sub-grid tensors (batch B*D)
   int64_t w_off = 0, b_off = 0;
   Dims in, out;
@@ -228,6 +229,9 @@ void set_pw(ConvLayer &L, const Dims &in, int cin_total) {
     if (L.K[i] != 1 || L.S[i] != 1 || L.P[i] != 0) return;
   L.pw = pw_supported(in.Cs, L.out.Cs, L.Cout, false) &&
          (!L.has_dgrad || pw_supported(in.Cs, L.out.Cs, L.Cout, true));
+  // (the slab layout is bwgrad's taps_rows one, planned in L.wg)
+  L.pw_wg = L.wg.use_bw && L.wg.taps_rows && L.wg.ACs == in.Cs && L.wg.GCs == L.out.Cs &&
+            pw_wgrad_supported(in.Cs, L.out.Cs);
 }
 
 // Conv3d with stride / zero padding (nn.Conv3d(..., stride, padding), the
@@ -1132,8 +1136,28 @@ int conv_wgrad(Ctx &c, const ConvLayer &L, const float *A, const float *asc, con
   w.a_scale = asc;
   w.a_shift = ash;
   w.G = dy;
-  if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
-  if (int e = launch_wgrad(w, c.wstream())) return e;
+  if (L.pw_wg && !asc) {   // 1x1x1 without a BatchNorm input: the VALU form (pwconv.hip)
+    const long nvox = L.out.vox();
+    w.KB = pw_wgrad_blocks(nvox);
+    if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
+    PwWgArgs pa{};
+    pa.A = reinterpret_cast<const uint16_t *>(A);
+    pa.G = reinterpret_cast<const uint16_t *>(dy);
+    pa.partial = w.partial;
+    pa.nvox = nvox;
+    pa.per_block = (nvox + w.KB - 1) / w.KB;
+    pa.ACs = w.ACs;
+    pa.GCs = w.GCs;
+    pa.ACR = w.ACr > 0 ? w.ACr : w.ACs;
+    pa.GCR = w.GCr > 0 ? w.GCr : w.GCs;
+    pa.Mtot = w.Mtot;
+    pa.Ntot = w.Ntot;
+    pa.bias_row = w.bias_row;
+    if (int e = launch_pw_wgrad(pa, w.KB, c.wstream())) return e;
+  } else {
+    if (int e = c.slab(wgrad_partial_floats(w), w.partial)) return e;
+    if (int e = launch_wgrad(w, c.wstream())) return e;
+  }
   WGradFinalize f{};
   f.partial = w.partial;
   f.dw = c.G + L.w_off;
