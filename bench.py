@@ -127,6 +127,10 @@ def tagify(rocprof_name):
     if n.startswith('bconv_kernel<') and n.count(',') == 5:
         # the fused-BatchNorm-backward flag is an int template argument there
         n = re.sub(r',0>$', '>', re.sub(r',1>$', ',bnb>', n))
+    m = re.match(r'^bwgrad_pipe_kernel<(\d+),(\d+),(\d+),(\d+)>$', n)
+    if m and m.group(1) != '32' and m.group(3) == m.group(4):
+        # equal A / G prefetch depths are timed as <MSW,NS,NP> (bwgrad.hip BWP)
+        n = 'bwgrad_pipe_kernel<%s,%s,%s>' % m.group(1, 2, 3)
     return n
 
 
