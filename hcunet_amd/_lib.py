@@ -140,6 +140,10 @@ SYMBOLS = [
     ("hcu_resid_fwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_resid_bwd", _I, [_VP, _VP, _VP, _VP, _I64, _VP]),
     ("hcu_sum_parts", _I, [ctypes.POINTER(_VP), _I, _VP, _I64, _I, _VP]),
+    ("hcu_pw_conv_forward", _I, [ctypes.POINTER(_VP), _I, _I, _I, _VP, _VP, _VP, _I64, _I, _I, _VP]),
+    ("hcu_pw_conv_work_floats", _SZ, [_I64, _I, _I, _I]),
+    ("hcu_pw_conv_backward", _I, [ctypes.POINTER(_VP), _I, _I, _I, _VP, _VP, _I, _I, ctypes.POINTER(_VP),
+                                  _VP, _VP, _I64, _VP, _SZ, _I, _VP]),
     ("hcu_unet_set_grad_events", _I, [_VP, _VP, _VP, _I]),
     ("hcu_unet_grad_events_live", _I, [_VP]),
     ("hcu_event_create", _I, [ctypes.POINTER(_VP)]),
@@ -236,6 +240,13 @@ def stream_handle(device=None):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def env_flag(name, default):
+    """An on/off switch of the environment (A/B runs): '0' is off, any
+    other value on, unset `default`."""
+    v = os.environ.get(name)
+    return default if v is None or v == '' else v != '0'
 
 
 def require_device(t, what):

@@ -399,12 +399,19 @@ struct WGradArgs {
 // the PyTorch layout [Cout][Cin]; part_c / part_cs: ConvLayer's channel parts.
 //   dgrad 0: in [nvox][ICs] -> out [nvox][OCs] (+ bias)
 //   dgrad 1: in = dy [nvox][ICs = the forward's OCs] -> out = dx [nvox][OCs = the forward's ICs]
+//   nparts > 0: the slot-strided side (the forward's input, the dgrad's
+//   output) is nparts separate tensors [nvox][pcs] instead of one [nvox][ICs
+//   | OCs] (RDCNet's channel cats, never materialised: hcu_pw_conv_*)
+constexpr int kPwMaxParts = 8;
 struct PwArgs {
   const uint16_t *in;
   const float *w, *bias;
   uint16_t *out;
   long nvox;
   int ICs, OCs, Cin, Cout, part_c, part_cs, dgrad;
+  int nparts, pcs;
+  const uint16_t *inp[kPwMaxParts];
+  uint16_t *outp[kPwMaxParts];
 };
 bool pw_supported(int ICs, int OCs, int Cout, bool dgrad);
 int launch_pw(const PwArgs &a, hipStream_t s);
@@ -416,6 +423,8 @@ struct PwWgArgs {
   float *partial;
   long nvox, per_block;
   int ACs, GCs, ACR, GCR, Mtot, Ntot, bias_row;
+  int nparts, pcs;                      // nparts > 0: A is nparts tensors [nvox][pcs] (Ap)
+  const uint16_t *Ap[kPwMaxParts];
 };
 bool pw_wgrad_supported(int ACs, int GCs);
 int pw_wgrad_blocks(long nvox);

@@ -19,9 +19,11 @@
 //   forward:  out[v][o] = bias[o] + sum_e in[v][e] * W[o][torch(e)]
 //   dgrad:    dx[v][e]  = sum_o dy[v][o] * W[o][torch(e)]
 // fp32 accumulation in K-step order; 0 in every padding slot of the output.
+#include "hcunet.h"
 #include "common.h"
 #include "timing.h"
 #include <algorithm>
+#include <string>
 
 namespace hcu {
 
@@ -38,7 +40,9 @@ __device__ __forceinline__ int pw_torch_channel(int e, int Cin, int part_c, int 
 
 // KS K-steps of 32 input slots, NS output subtiles of 16, G voxel groups of 16
 // per wave iteration (their loads issued together).
-template <int KS, int NS, int G>
+// PM: 0 one tensor on each side; 1 the forward's input is channel parts
+// (loads); 2 the input gradient's output is channel parts (stores).
+template <int KS, int NS, int G, int PM>
 __global__ void __launch_bounds__(256) pw_kernel(const PwArgs a) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15, kq = lane >> 4;
@@ -81,6 +85,26 @@ __global__ void __launch_bounds__(256) pw_kernel(const PwArgs a) {
   // (num_records = the tensor's bytes: the 0x7ffffff0 sentinel lies past it)
   const __amdgpu_buffer_rsrc_t rin =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, (int)(a.nvox * a.ICs * 2), 0x00020000);
+  // parts form (a.nparts > 0): the slot-strided side is the forward's input
+  // (pin: loads) or the input gradient's output (pout: stores).  pin: this
+  // lane's slot c of K step ks lives in part c / pcs at offset c % pcs of its
+  // [nvox][pcs] rows.  (The dgrad's input is the one dy tensor.)
+  constexpr bool pin = PM == 1, pout = PM == 2;
+  const uint16_t *pbase[KS];
+  int poff[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const int c = ks * 32 + 8 * kq;
+    const int pi = pin ? c / a.pcs : 0;
+    const uint16_t *b0 = a.inp[0];
+    if constexpr (pin) {
+#pragma unroll
+      for (int q = 1; q < kPwMaxParts; ++q)
+        if (pi == q) b0 = a.inp[q];
+    }
+    pbase[ks] = b0;
+    poff[ks] = pin ? c - pi * a.pcs : 0;
+  }
   for (long g0 = wave * G; g0 < ngroups; g0 += nwaves * G) {
     shortx8 b[G][KS];
 #pragma unroll
@@ -91,6 +115,13 @@ __global__ void __launch_bounds__(256) pw_kernel(const PwArgs a) {
       for (int ks = 0; ks < KS; ++ks) {
         const int c = ks * 32 + 8 * kq;
         const bool ok = vok && c < a.ICs;
+        if constexpr (pin) {
+          // (the address stays inside part 0's first row when !ok; the value is zeroed)
+          const uint16_t *ptr = ok ? pbase[ks] + v * a.pcs + poff[ks] : a.inp[0];
+          const uint4 w = *reinterpret_cast<const uint4 *>(ptr);
+          b[gi][ks] = __builtin_bit_cast(shortx8, ok ? w : make_uint4(0u, 0u, 0u, 0u));
+          continue;
+        }
         // (64-bit voxel base folded into the resource would need a descriptor
         // per group; the tensors here stay below 2 GiB: launch_pw checks)
         const int off = ok ? (int)((v * a.ICs + c) * 2) : 0x7ffffff0;
@@ -115,6 +146,15 @@ __global__ void __launch_bounds__(256) pw_kernel(const PwArgs a) {
         if (c0 >= a.OCs) continue;
         const uint2 w = make_uint2(pack_bf2(acc[ns][0] + bias[ns][0], acc[ns][1] + bias[ns][1]),
                                    pack_bf2(acc[ns][2] + bias[ns][2], acc[ns][3] + bias[ns][3]));
+        if constexpr (pout) {   // slot c0 of part c0 / pcs
+          const int pi = c0 / a.pcs;
+          uint16_t *o = a.outp[0];
+#pragma unroll
+          for (int q = 1; q < kPwMaxParts; ++q)
+            if (pi == q) o = a.outp[q];
+          *reinterpret_cast<uint2 *>(o + v * a.pcs + (c0 - pi * a.pcs)) = w;
+          continue;
+        }
         *reinterpret_cast<uint2 *>(a.out + v * a.OCs + c0) = w;
       }
     }
@@ -164,9 +204,19 @@ __global__ void __launch_bounds__(256) pw_wgrad_kernel(const PwWgArgs a) {
         const bool isA = i < nA;
         const int ii = isA ? i : i - nA, per = isA ? E8 : G8;
         const int v = ii / per, q = ii - v * per;
-        if (c0 + v < v1)
-          w = isA ? *reinterpret_cast<const uint4 *>(a.A + (c0 + v) * a.ACs + q * 8)
-                  : *reinterpret_cast<const uint4 *>(a.G + (c0 + v) * a.GCs + q * 8);
+        if (c0 + v < v1) {
+          if (isA && a.nparts > 0) {   // slot q*8 of part q*8 / pcs
+            const int pi = q * 8 / a.pcs;
+            const uint16_t *pa = a.Ap[0];
+#pragma unroll
+            for (int t = 1; t < kPwMaxParts; ++t)
+              if (pi == t) pa = a.Ap[t];
+            w = *reinterpret_cast<const uint4 *>(pa + (c0 + v) * a.pcs + (q * 8 - pi * a.pcs));
+          } else {
+            w = isA ? *reinterpret_cast<const uint4 *>(a.A + (c0 + v) * a.ACs + q * 8)
+                    : *reinterpret_cast<const uint4 *>(a.G + (c0 + v) * a.GCs + q * 8);
+          }
+        }
       }
       rr[k] = w;
     }
@@ -276,14 +326,19 @@ int launch_pw(const PwArgs &a, hipStream_t s) {
   const double fl = 2.0 * a.nvox * (double)a.Cin * a.Cout;
   const double by = 2.0 * a.nvox * (double)(a.ICs + a.OCs);
   bool ok = false;
-#define PW(KS_, NS_)                                                                              \
-  if (!ok && KS == KS_ && NS == NS_) {                                                            \
-    HCU_TIMED(s, "pw_kernel<" #KS_ "," #NS_ ">", fl, by,                                          \
-              HCU_LAUNCH((pw_kernel<KS_, NS_, G>), dim3(grid), dim3(256), 0, s, a));              \
+  const int PM = a.nparts > 0 ? (a.dgrad ? 2 : 1) : 0;
+#define PW(KS_, NS_, PM_)                                                                         \
+  if (!ok && KS == KS_ && NS == NS_ && PM == PM_) {                                               \
+    HCU_TIMED(s, PM_ ? "pw_kernel<" #KS_ "," #NS_ ",parts>" : "pw_kernel<" #KS_ "," #NS_ ">", fl, by, \
+              HCU_LAUNCH((pw_kernel<KS_, NS_, G, PM_>), dim3(grid), dim3(256), 0, s, a));         \
     ok = true;                                                                                    \
   }
-  PW(1, 1) PW(2, 1) PW(3, 1) PW(4, 1) PW(1, 2) PW(2, 2) PW(3, 2) PW(4, 2)
-  PW(1, 3) PW(1, 4) PW(1, 5) PW(1, 6)
+  PW(1, 1, 0) PW(2, 1, 0) PW(3, 1, 0) PW(4, 1, 0) PW(1, 2, 0) PW(2, 2, 0) PW(3, 2, 0) PW(4, 2, 0)
+  PW(1, 3, 0) PW(1, 4, 0) PW(1, 5, 0) PW(1, 6, 0)
+  // the channel-parts forms (hcu_pw_conv_*): forward K <= 96 slots into <= 16
+  // channels, input gradient <= 16 channels into <= 96 slots
+  PW(1, 1, 1) PW(2, 1, 1) PW(3, 1, 1) PW(1, 2, 1) PW(2, 2, 1) PW(3, 2, 1) PW(1, 1, 2) PW(1, 2, 2) PW(1, 3, 2) PW(1, 4, 2) PW(1, 5, 2)
+  PW(1, 6, 2)
 #undef PW
   if (!ok) return fail(4, "pwconv: unsupported channel counts");
   HCU_CHECK_LAUNCH();
@@ -291,3 +346,122 @@ int launch_pw(const PwArgs &a, hipStream_t s) {
 }
 
 }  // namespace hcu
+
+// ---------------------------------------------------------------------------
+// C-ABI (include/hcunet.h): the cat + 1x1x1 convolution of RDCNet's
+// recurrence on the separate channel parts (no cat, no split).
+namespace {
+int pw_check(const void *const *parts, int nparts, int part_c, int part_cs, int64_t nvox, int Cout,
+             int out_cs, const char *who) {
+  if (!parts || nparts < 1 || nparts > hcu::kPwMaxParts || part_c < 1 || part_cs % 8 || part_c > part_cs ||
+      Cout < 1 || out_cs % 8 || Cout > out_cs || nvox < 0)
+    return hcu::fail(1, std::string(who) + ": 1..8 parts of part_cs (a multiple of 8) slots, Cout <= out_cs");
+  for (int i = 0; i < nparts; ++i)
+    if (!parts[i] || reinterpret_cast<uintptr_t>(parts[i]) % 16)
+      return hcu::fail(1, std::string(who) + ": parts must be non-null and 16-byte aligned");
+  if (!hcu::pw_supported(nparts * part_cs, out_cs, Cout, false) ||
+      !hcu::pw_supported(nparts * part_cs, out_cs, Cout, true) ||
+      !hcu::pw_wgrad_supported(nparts * part_cs, out_cs))
+    return hcu::fail(4, std::string(who) + ": unsupported channel counts");
+  return 0;
+}
+}  // namespace
+
+extern "C" int hcu_pw_conv_forward(const void *const *parts, int nparts, int part_c, int part_cs, const float *w,
+                                   const float *b, void *out, int64_t nvox, int Cout, int out_cs, void *stream) {
+  if (int e = pw_check(parts, nparts, part_c, part_cs, nvox, Cout, out_cs, "hcu_pw_conv_forward")) return e;
+  if (!w || !out) return hcu::fail(1, "hcu_pw_conv_forward: null weight or output");
+  if (nvox == 0) return 0;
+  hcu::PwArgs a{};
+  a.in = static_cast<const uint16_t *>(parts[0]);
+  a.w = w;
+  a.bias = b;
+  a.out = static_cast<uint16_t *>(out);
+  a.nvox = nvox;
+  a.ICs = nparts * part_cs;
+  a.OCs = out_cs;
+  a.Cin = nparts * part_c;
+  a.Cout = Cout;
+  a.part_c = part_c;
+  a.part_cs = part_cs;
+  a.nparts = nparts;
+  a.pcs = part_cs;
+  for (int i = 0; i < nparts; ++i) a.inp[i] = static_cast<const uint16_t *>(parts[i]);
+  return hcu::launch_pw(a, (hipStream_t)stream);
+}
+
+extern "C" size_t hcu_pw_conv_work_floats(int64_t nvox, int nparts, int part_cs, int Cout) {
+  return (size_t)hcu::pw_wgrad_blocks(nvox) * ((size_t)nparts * part_cs + 1) * Cout;
+}
+
+extern "C" int hcu_pw_conv_backward(const void *const *parts, int nparts, int part_c, int part_cs, const float *w,
+                                    const void *dout, int Cout, int out_cs, void *const *dparts, float *dw,
+                                    float *db, int64_t nvox, float *work, size_t work_floats, int accumulate,
+                                    void *stream) {
+  if (int e = pw_check(parts, nparts, part_c, part_cs, nvox, Cout, out_cs, "hcu_pw_conv_backward")) return e;
+  if (!w || !dout || !dw || !work) return hcu::fail(1, "hcu_pw_conv_backward: null weight, gradient or workspace");
+  if (work_floats < hcu_pw_conv_work_floats(nvox, nparts, part_cs, Cout))
+    return hcu::fail(1, "hcu_pw_conv_backward: workspace too small (hcu_pw_conv_work_floats)");
+  hipStream_t s = (hipStream_t)stream;
+  const int ACs = nparts * part_cs, Cin = nparts * part_c;
+  if (dparts) {   // input gradients, straight into the parts' layout
+    hcu::PwArgs a{};
+    a.in = static_cast<const uint16_t *>(dout);
+    a.w = w;
+    a.nvox = nvox;
+    a.ICs = out_cs;
+    a.OCs = ACs;
+    a.Cin = Cin;
+    a.Cout = Cout;
+    a.part_c = part_c;
+    a.part_cs = part_cs;
+    a.dgrad = 1;
+    a.nparts = nparts;
+    a.pcs = part_cs;
+    for (int i = 0; i < nparts; ++i) {
+      if (!dparts[i] || reinterpret_cast<uintptr_t>(dparts[i]) % 16)
+        return hcu::fail(1, "hcu_pw_conv_backward: input gradients must be non-null and 16-byte aligned");
+      a.outp[i] = static_cast<uint16_t *>(dparts[i]);
+    }
+    a.out = a.outp[0];
+    if (nvox > 0)
+      if (int e = hcu::launch_pw(a, s)) return e;
+  }
+  // weight / bias gradient: slabs (one per block) + the fixed-order finalize
+  const int KB = hcu::pw_wgrad_blocks(nvox);
+  hcu::PwWgArgs g{};
+  g.G = static_cast<const uint16_t *>(dout);
+  g.A = static_cast<const uint16_t *>(parts[0]);
+  g.partial = work;
+  g.nvox = nvox;
+  g.per_block = (nvox + KB - 1) / KB;
+  g.ACs = ACs;
+  g.GCs = out_cs;
+  g.ACR = ACs;   // (slots: the finalize maps torch channels to them)
+  g.GCR = Cout;
+  g.Mtot = ACs + 1;
+  g.Ntot = Cout;
+  g.bias_row = 1;
+  g.nparts = nparts;
+  g.pcs = part_cs;
+  for (int i = 0; i < nparts; ++i) g.Ap[i] = static_cast<const uint16_t *>(parts[i]);
+  if (int e = hcu::launch_pw_wgrad(g, KB, s)) return e;
+  hcu::WGradFinalize f{};
+  f.partial = work;
+  f.dw = dw;
+  f.db = db;
+  f.KB = KB;
+  f.Mtot = g.Mtot;
+  f.Ntot = g.Ntot;
+  f.T = 1;
+  f.mode = 0;
+  f.Cout = Cout;
+  f.Cin_g = Cin;
+  f.groups = 1;
+  f.fold_mod = Cin;
+  f.part_c = part_c;
+  f.part_cs = part_cs;
+  f.ACs = ACs;
+  f.accumulate = accumulate;
+  return hcu::launch_wgrad_finalize(f, s);
+}

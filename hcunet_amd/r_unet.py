@@ -31,7 +31,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .chain import Chain, bf16_active, flat_of, upsample_cat_check
+from . import chain as _chain_mod
+from .chain import Chain, bf16_active, cl_channels, flat_of, upsample_cat_check
 
 
 def crop(x, y):
@@ -191,6 +192,87 @@ class _Resid(torch.autograd.Function):
         _lib.check(_lib.lib().hcu_resid_bwd(_lib.ptr(g32), _lib.ptr(gc), _lib.ptr(dy), _lib.ptr(dm), dy.numel(),
                                             _lib.stream_handle(dy.device)), 'residual add backward')
         return dm, dy
+
+
+class _PwConv(torch.autograd.Function):
+    """cat(parts, -1) -> 1x1x1 Conv3d (no BatchNorm) on bf16 channels-last
+    channel parts, without the cat (hcat/r_unet.py:223 cat(x, y) ->
+    RDCBlock.conv, :362 the dilated branches' cat -> StackedDilation.out_conv):
+    hcu_pw_conv_forward / _backward read and write the parts where they are.
+    The weight and bias gradients accumulate into the flat gradient buffer the
+    layer chains of the same root use (FlatParams.grad_target)."""
+
+    @staticmethod
+    def forward(ctx, conv, flat, part_c, weight, *parts):
+        parts = [p.contiguous() for p in parts]
+        p0 = parts[0]
+        nvox = p0.numel() // p0.shape[-1]
+        cout = conv.out_channels
+        ocs = cl_channels(cout, True)
+        out = torch.empty(tuple(p0.shape[:-1]) + (ocs,), dtype=torch.bfloat16, device=p0.device)
+        ptrs = (ctypes.c_void_p * len(parts))(*[p.data_ptr() for p in parts])
+        _lib.check(_lib.lib().hcu_pw_conv_forward(ptrs, len(parts), part_c, p0.shape[-1], _lib.ptr(conv.weight),
+                                                  _lib.ptr(conv.bias), _lib.ptr(out), nvox, cout, ocs,
+                                                  _lib.stream_handle(p0.device)), '1x1x1 convolution')
+        ctx.conv, ctx.flat, ctx.part_c = conv, flat, part_c
+        ctx.key = _pw_key(conv)
+        ctx.save_for_backward(*parts)
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dout):
+        parts = ctx.saved_tensors
+        conv, flat = ctx.conv, ctx.flat
+        if _pw_key(conv) != ctx.key:
+            raise RuntimeError('hcunet_amd: a parameter of %r was modified between its forward and its '
+                               'backward' % conv)
+        p0 = parts[0]
+        dev = p0.device
+        dout = dout.contiguous().to(torch.bfloat16)
+        nvox = p0.numel() // p0.shape[-1]
+        cout = conv.out_channels
+        ocs = dout.shape[-1]
+        L = _lib.lib()
+        need = any(ctx.needs_input_grad[4:])
+        dparts = [torch.empty_like(p) for p in parts] if need else None
+        G, finish = flat.grad_target()
+        base = G.data_ptr()
+        dw = ctypes.c_void_p(base + 4 * flat.offset(conv.weight))
+        db = ctypes.c_void_p(base + 4 * flat.offset(conv.bias)) if conv.bias is not None else ctypes.c_void_p()
+        nw = int(L.hcu_pw_conv_work_floats(nvox, len(parts), p0.shape[-1], cout))
+        work = torch.empty(max(nw, 1), dtype=torch.float32, device=dev)
+        ptrs = (ctypes.c_void_p * len(parts))(*[p.data_ptr() for p in parts])
+        dptrs = (ctypes.c_void_p * len(parts))(*[d.data_ptr() for d in dparts]) if need else None
+        _lib.check(L.hcu_pw_conv_backward(ptrs, len(parts), ctx.part_c, p0.shape[-1], _lib.ptr(conv.weight),
+                                          ctypes.c_void_p(dout.data_ptr()), cout, ocs, dptrs, dw, db, nvox,
+                                          ctypes.c_void_p(work.data_ptr()), nw, 1, _lib.stream_handle(dev)),
+                   '1x1x1 convolution backward')
+        finish()
+        return (None, None, None, None) + (tuple(dparts) if need else (None,) * len(parts))
+
+
+def _pw_key(conv):
+    return (_chain_mod._WEIGHT_EPOCH[0], conv.weight._version,
+            conv.bias._version if conv.bias is not None else -1)
+
+
+def pw_conv(conv, root, part_c, parts):
+    """The cat of channels-last bf16 parts [..., cl_channels(part_c)] followed
+    by the bias-carrying 1x1x1 `conv` of module tree `root`, as one native op
+    (_PwConv); None when the shapes are not the ones it takes (the caller then
+    runs cl_cat + the layer chain)."""
+    p0 = parts[0]
+    pcs = cl_channels(part_c, True)
+    k = conv.kernel_size if isinstance(conv.kernel_size, tuple) else (conv.kernel_size,) * 3
+    if (not p0.is_cuda or p0.dtype != torch.bfloat16 or tuple(k) != (1, 1, 1) or conv.groups != 1
+            or tuple(conv.stride) != (1, 1, 1) or tuple(conv.padding) != (0, 0, 0)
+            or conv.in_channels != part_c * len(parts) or not 1 <= len(parts) <= 8
+            or any(p.dtype != torch.bfloat16 or p.shape != p0.shape or p.device != p0.device for p in parts)
+            or p0.shape[-1] != pcs or len(parts) * pcs > 96 or cl_channels(conv.out_channels, True) > 32):
+        return None
+    flat = flat_of(root).ready()
+    return _PwConv.apply(conv, flat, part_c, conv.weight, *parts)
 
 
 def resid_add(m, y):
@@ -540,9 +622,18 @@ class RDCNet(nn.Module):
         yc = y.to(x.dtype)                             # y in the compute dtype (the cat's / out_conv's input)
         trace = getattr(self, '_y_trace', None)   # (tests: y after every recurrence step)
         xs = fan(x, 10)
+        # the bf16 path: the two cats and their 1x1x1 convolutions as one native
+        # op each (pw_conv: the parts are read where they are; HCU_PW_CAT=0 --
+        # or HCU_PW=0, which also takes the chains off the pointwise kernels --
+        # keeps cl_cat + the chains)
+        pw = bf16 and _lib.env_flag('HCU_PW', True) and _lib.env_flag('HCU_PW_CAT', True)
         for t in range(10):
-            h = fan(step(cl_cat([xs[t], yc]), tr, bf16), len(dil))
-            y, yc = resid_add(mix(cl_cat([d(hi, tr, bf16) for d, hi in zip(dil, h)]), tr, bf16), y)
+            s_in = [xs[t], yc]
+            u = pw_conv(blk.conv, self, C, s_in) if pw else None
+            h = fan(u if u is not None else step(cl_cat(s_in), tr, bf16), len(dil))
+            d_out = [d(hi, tr, bf16) for d, hi in zip(dil, h)]
+            m = pw_conv(sd.out_conv, self, C, d_out) if pw else None
+            y, yc = resid_add(m if m is not None else mix(cl_cat(d_out), tr, bf16), y)
             if trace is not None:
                 trace.append(y.detach().clone())
         if bf16:

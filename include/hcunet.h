@@ -267,6 +267,25 @@ int hcu_cl_cat(void *const *parts, const int *part_row_bytes, int nparts, void *
 int hcu_resid_fwd(const void *m, const float *y, float *out, void *out_c, int64_t n, hcu_stream_t stream);
 int hcu_resid_bwd(const float *g32, const void *gc, float *dy, void *dm, int64_t n, hcu_stream_t stream);
 
+/* The channel cat + 1x1x1 Conv3d (no BatchNorm) of RDCNet's recurrence on
+ * bf16 channels-last channel parts, without the cat: hcat/r_unet.py:223
+ * cat(x, y) -> RDCBlock.conv (:372-374) and :362 the cat of the dilated
+ * branches -> StackedDilation.out_conv (:354-364), with their autograd
+ * backward.  parts[i]: [nvox][part_cs] bf16 with part_c real channels
+ * (Cin = nparts * part_c, 1..8 parts, part_cs a multiple of 8, 16-byte
+ * aligned); w: the PyTorch weight [Cout][Cin] fp32, b: [Cout] or NULL; out /
+ * dout: [nvox][out_cs] bf16 (out_cs = Cout rounded up to 8, padding 0).
+ * Backward: dparts (NULL: no input gradients) in the parts' layout; dw / db
+ * (db nullable) overwritten or, accumulate != 0, added to; work: scratch of
+ * hcu_pw_conv_work_floats(...) floats.  Channel counts: nparts * part_cs <= 96
+ * slots, out_cs <= 32. */
+int hcu_pw_conv_forward(const void *const *parts, int nparts, int part_c, int part_cs, const float *w,
+                        const float *b, void *out, int64_t nvox, int Cout, int out_cs, hcu_stream_t stream);
+size_t hcu_pw_conv_work_floats(int64_t nvox, int nparts, int part_cs, int Cout);
+int hcu_pw_conv_backward(const void *const *parts, int nparts, int part_c, int part_cs, const float *w,
+                         const void *dout, int Cout, int out_cs, void *const *dparts, float *dw, float *db,
+                         int64_t nvox, float *work, size_t work_floats, int accumulate, hcu_stream_t stream);
+
 /* out = parts[0] + parts[1] + ... (n elements, fp32 accumulation in input
  * order, one rounding; bf = 1: bf16 tensors, else fp32; NULL parts skipped;
  * at most 16).  The gradient of a tensor read by several chains (RDCNet:

@@ -503,3 +503,32 @@ def test_rdcnet_bf16_weight_gradient_all_taps_matches_split(tmp_path, shape):
         if not r <= 1e-4:
             bad.append((k, r))
     assert not bad, bad
+
+
+def test_rdcnet_bf16_cat_free_mixing_matches_cat_and_chain(monkeypatch):
+    """The bf16 RDCNet recurrence's two channel cats + 1x1x1 convolutions as
+    one native op each (r_unet.pw_conv: hcu_pw_conv_forward / _backward on
+    the separate parts) against cl_cat + the layer chain (HCU_PW_CAT=0, the
+    chain's own pointwise kernels): the same kernels and summation order, so
+    the output, the loss and every gradient must be bitwise equal."""
+    torch.manual_seed(3)
+    net = RDCNet(4, 5).cuda().train()
+    shape = (1, 4, 64, 48, 24)
+    x = torch.from_numpy(inputs.make_x(shape)).cuda()
+    mshape = (1, 1) + shape[2:]
+    mask = torch.from_numpy(inputs.make_mask(mshape)).cuda()
+    pwl = torch.from_numpy(inputs.make_pwl(mshape)).cuda()
+    res = {}
+    for arm in ('0', '1'):
+        monkeypatch.setenv('HCU_PW_CAT', arm)
+        net.zero_grad(set_to_none=True)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = net(x)
+            loss = hl.cross_entropy(out[:, 0:1], mask, pwl, method='pixel')
+        loss.backward()
+        torch.cuda.synchronize()
+        res[arm] = (out.detach().cpu(), loss.item(), [p.grad.detach().cpu().clone() for p in net.parameters()])
+    (o0, l0, g0), (o1, l1, g1) = res['0'], res['1']
+    assert torch.equal(o0, o1) and l0 == l1
+    for (k, _), a, b in zip(net.named_parameters(), g0, g1):
+        assert torch.equal(a, b), k
