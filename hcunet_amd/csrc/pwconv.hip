@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(256) pw_kernel(const PwArgs a) {
 // for one voxel subset; the subsets are summed in a fixed order at the end
 // and the block writes one slab in bwgrad's taps_rows layout (WGradArgs Mtot
 // / Ntot / ACr / GCr, bias row last) for wgrad_finalize.
-constexpr int kPwNV = 64;        // voxels per chunk
+constexpr int kPwNV = 64;        // voxels per chunk (128 chunks at 184 VGPRs, 2 blocks per CU: slower)
 constexpr int kPwLoads = 4;      // 16-byte staging loads per thread and chunk (A + G)
 
 __global__ void __launch_bounds__(256) pw_wgrad_kernel(const PwWgArgs a) {
@@ -295,9 +295,14 @@ bool pw_wgrad_supported(int ACs, int GCs) {
 
 int pw_wgrad_blocks(long nvox) {
   // one resident round: 136 VGPRs leave 3 waves per SIMD = 3 blocks per CU
-  // (1024 blocks ran a second round of 256: 62 vs ~31 us), >= 4 chunks a block
+  // (1024 blocks ran a second round of 256: 62 vs ~31 us), >= 4 chunks a
+  // block.  HCU_PW_WG_BLOCKS: the cap (A/B)
+  static const long cap = [] {
+    const char *e = getenv("HCU_PW_WG_BLOCKS");
+    return e && atoi(e) > 0 ? (long)atoi(e) : 768L;
+  }();
   const long b = (nvox + 4 * kPwNV - 1) / (4 * kPwNV);
-  return (int)std::max(1L, std::min(b, 768L));
+  return (int)std::max(1L, std::min(b, cap));
 }
 
 int launch_pw_wgrad(const PwWgArgs &a, int blocks, hipStream_t s) {
