@@ -503,6 +503,16 @@ static long conv8_lds(const GConvArgs &a, int C4, int HVP, int G) {
          (long)sizeof(GConvArgs);   // + the static copy of the arguments
 }
 
+// HCU_CONV8_NPF: the prefetch limit (elements per thread) at G <= 4.  12 by
+// default: config 2's d1.c1 input gradient then takes G = 2 with 12 prefetched
+// elements, 63.9 us, against G = 4 with 16 at 69.6 us (round 5's limit 16;
+// config 2, 5 interleaved runs each: 1.919-1.929 vs 1.925-1.941 ms/step)
+static int env_npf_max() {
+  const char *e = getenv("HCU_CONV8_NPF");
+  const int v = e ? atoi(e) : 12;
+  return v == 16 ? 16 : 12;
+}
+
 // Chooses the tile, groups per wave and grid for conv8_kernel; non-zero when
 // the shape is not one conv8 handles (the caller then plans conv2 / gconv).
 int plan_conv8(GConvArgs &a, int target_blocks) {
@@ -537,10 +547,9 @@ int plan_conv8(GConvArgs &a, int target_blocks) {
     const long lds = conv8_lds(a, C4, HVP, G);
     const long tiles = (long)a.B * cdiv(a.OX, TX) * cdiv(a.OY, TY) * ntz;
     // two workgroups per CU; <= 12 prefetched elements per thread at G = 8
-    // (16 spills registers there), <= 16 at G <= 4: config 2's d1.c1 input
-    // gradient then takes G = 4 (62 -> 54 us; the step, branch-bound there,
-    // unchanged: 1.958-1.971 vs 1.959-1.965 ms)
-    if (lds > 80 * 1024 || HV * C4 > (G <= 4 ? 16 : 12) * 256) continue;
+    // (16 spills registers there); at G <= 4 the limit of env_npf_max()
+    static const int npf_max = env_npf_max();
+    if (lds > 80 * 1024 || HV * C4 > (G <= 4 ? npf_max : 12) * 256) continue;
     a.G8 = G;
     a.TX = TX;
     a.TY = TY;
