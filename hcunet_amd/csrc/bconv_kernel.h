@@ -358,8 +358,12 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   // channels (fetch_adv) instead of re-deriving the tile origin and the
   // element addresses from the LDS copy of the arguments (~1.5 K cycles per
   // chunk in the deep levels' multi-chunk tiles)
+  // (not in the fused-BatchNorm-backward instances with 12+ prefetched
+  // elements: at 256 VGPRs the 12 saved offsets cost config 3's d0.c2 input
+  // gradient 303 -> 340 us, and its tiles are single-chunk)
+  constexpr bool ADV = !NCX && !(BNB && NPF >= 12);
   __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc((void *)a.in, 0, 0, 0x00020000);
-  int foff[NPFR];
+  int foff[ADV ? NPFR : 1];
   // halo of (tile, chunk) -> pf (branch-free: the validity of each element is
   // a mask, invalid elements read offset 0x7ffffff0, outside the buffer -> 0)
   // NCXYZ input (NCX): element u's channels from the planes; the raw loaded
@@ -413,14 +417,14 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
                       ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
-      foff[u] = off;
+      if constexpr (ADV) foff[u] = off;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
-    frs = rs;
+    if constexpr (ADV) frs = rs;
   };
   auto fetch_adv = [&]() {   // the next channel chunk of the tile just fetched
-    if constexpr (!NCX) {
+    if constexpr (ADV) {
 #pragma unroll
       for (int u = 0; u < NPFR; ++u) {
         foff[u] += ((okbits >> u) & 1u) ? CK * ES : 0;
@@ -459,11 +463,11 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
                       ((unsigned)gz < (unsigned)IZ);
       const int off = ok ? base_off + (int)(__umul24(hx, bX) + __umul24(hy, bY) + __umul24(hz, bZ))
                          : 0x7ffffff0;
-      foff[u] = off;
+      if constexpr (ADV) foff[u] = off;
       pf[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       okbits |= (uint32_t)ok << u;
     }
-    frs = rs;
+    if constexpr (ADV) frs = rs;
   };
   auto load_coefs = [&]() {
     for (int j = tid; j < NT; j += 256) {
@@ -769,7 +773,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
           nt = tile + 1;
         }
         if (nt < t_end) {
-          if (nt == tile)
+          if (ADV && nt == tile)
             fetch_adv();
           else
             fetch(nt, nc);
