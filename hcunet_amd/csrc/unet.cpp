@@ -973,7 +973,10 @@ struct Ctx {
   }
   int flush_wgf() {
     int e = 0;
-    if (!pend.empty()) e = launch_wgrad_finalize_batch(pend.data(), (int)pend.size(), wstream());
+    // HCU_DEBUG_NO_WGF=1 drops every weight-gradient finalize: WRONG gradients,
+    // a timing probe only (what the finalizes cost a step)
+    static const bool no_wgf = getenv("HCU_DEBUG_NO_WGF") && getenv("HCU_DEBUG_NO_WGF")[0] == '1';
+    if (!pend.empty() && !no_wgf) e = launch_wgrad_finalize_batch(pend.data(), (int)pend.size(), wstream());
     pend.clear();
     wp_off = 0;
     return e;

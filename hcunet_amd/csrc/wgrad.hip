@@ -714,10 +714,15 @@ int launch_wgrad(const WGradArgs &a, hipStream_t s) {
 // fixed order.  The result is scattered into the PyTorch weight layout.
 // S == 0 selects the tiled form (wgrad_finalize_tile) for the large layers.
 __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int S, double *red);
+__device__ __forceinline__ void wgrad_finalize_body4(const WGradFinalize &f, int S, double *red);
+__device__ __forceinline__ void wgrad_finalize_emit(const WGradFinalize &f, int64_t idx, double s);
 __device__ __forceinline__ void wgrad_finalize_tile(const WGradFinalize &f, int bx, float (*tl)[33]);
 __global__ void __launch_bounds__(256) wgrad_finalize_kernel(const WGradFinalize f, int S) {
-  __shared__ double sh[528];   // red[256] (S > 0) or the 32 x 33 float tile (S == 0)
+  // red[256] (S > 0), red[4][256] (S < 0: the 16-byte form) or the 32 x 33
+  // float tile (S == 0)
+  __shared__ double sh[1024];
   if (S == 0) wgrad_finalize_tile(f, blockIdx.x, reinterpret_cast<float (*)[33]>(sh));
+  else if (S < 0) wgrad_finalize_body4(f, -S, sh);
   else wgrad_finalize_body(f, S, sh);
 }
 // Several layers' finalizes in one launch (grid.y = job): the backward defers
@@ -729,11 +734,51 @@ struct WGFBatch {
 };
 static_assert(sizeof(WGFBatch) <= 4000, "finalize batch must fit the 4 KB kernel-argument limit");
 __global__ void __launch_bounds__(256) wgrad_finalize_batch_kernel(const WGFBatch b) {
-  __shared__ double sh[528];
+  __shared__ double sh[1024];
   const int j = blockIdx.y;
   if ((int)blockIdx.x >= b.blocks[j]) return;
   if (b.S[j] == 0) wgrad_finalize_tile(b.f[j], blockIdx.x, reinterpret_cast<float (*)[33]>(sh));
+  else if (b.S[j] < 0) wgrad_finalize_body4(b.f[j], -b.S[j], sh);
   else wgrad_finalize_body(b.f[j], b.S[j], sh);
+}
+
+// The element-parallel sum with 16-byte slab reads: a thread owns 4
+// consecutive elements (four fp64 sums, each over k = sl, sl + S, ... in
+// increasing k, then the S partials combined in increasing sl -- the order of
+// wgrad_finalize_body, so the results are bitwise the same), and consecutive
+// threads read consecutive 16-byte groups of one slab (body's 4-byte reads
+// gave a wave 256 / S elements = 32 bytes of each slab at S = 32).
+__device__ __forceinline__ void wgrad_finalize_body4(const WGradFinalize &f, int S, double *red) {
+  const int64_t n = (int64_t)f.Mtot * f.Ntot;
+  const int TPG = 256 / S;   // threads per slab group
+  const int tid = threadIdx.x, el = tid % TPG, sl = tid / TPG;
+  const int64_t idx = ((int64_t)blockIdx.x * TPG + el) * 4;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (idx < n) {
+    const float4 *src = reinterpret_cast<const float4 *>(f.partial + idx);
+    const int64_t n4 = n / 4;
+#pragma unroll 4
+    for (int k = sl; k < f.KB; k += S) {
+      const float4 r = src[(size_t)k * n4];
+      a0 += (double)r.x;
+      a1 += (double)r.y;
+      a2 += (double)r.z;
+      a3 += (double)r.w;
+    }
+  }
+  red[tid] = a0;
+  red[256 + tid] = a1;
+  red[512 + tid] = a2;
+  red[768 + tid] = a3;
+  lds_barrier();
+  if (sl != 0 || idx >= n) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double *rq = red + q * 256;
+    double s = rq[el];
+    for (int j = 1; j < S; ++j) s += rq[j * TPG + el];
+    wgrad_finalize_emit(f, idx + q, s);
+  }
 }
 __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int S, double *red) {
   const int64_t n = (int64_t)f.Mtot * f.Ntot;
@@ -758,6 +803,12 @@ __device__ __forceinline__ void wgrad_finalize_body(const WGradFinalize &f, int 
   if (sl != 0 || idx >= n) return;
   double s = red[el];
   for (int j = 1; j < S; ++j) s += red[j * EPB + el];
+  wgrad_finalize_emit(f, idx, s);
+}
+
+// The finalized element idx of the slab sum s, scattered into PyTorch's layout.
+__device__ __forceinline__ void wgrad_finalize_emit(const WGradFinalize &f, int64_t idx, double s) {
+  const int64_t n = (int64_t)f.Mtot * f.Ntot;
   const float v = (float)s;
   const int grow = (int)(idx / f.Ntot), gcol = (int)(idx % f.Ntot);
   if (f.mode == 3) {   // ConvTranspose3d, phase form (WGradArgs::nph)
@@ -908,6 +959,15 @@ static void wgf_geometry(const WGradFinalize &f, int &S, int &blocks) {
   while (S < 64 && S * 2 <= f.KB && n * S / 256 < 1024) S *= 2;
   const int EPB = 256 / S;
   blocks = (int)((n + EPB - 1) / EPB);
+  // the 16-byte form (S < 0) for the sums whose slabs it can read as float4
+  // (same S, same order); HCU_WGF_VEC4=0 keeps the 4-byte form (A/B)
+  static const bool v4 = !(getenv("HCU_WGF_VEC4") && getenv("HCU_WGF_VEC4")[0] == '0');
+  if (v4 && S > 1 && tiled_finalize_mode() != 2 && (f.mode == 0 || f.mode == 1 || f.mode == 2) && n % 4 == 0 &&
+      reinterpret_cast<uintptr_t>(f.partial) % 16 == 0) {
+    blocks = (int)((n / 4 + EPB - 1) / EPB);
+    S = -S;
+    return;
+  }
   // large layers (no slab parallelism needed): the coalescing tiled form
   const int tm = tiled_finalize_mode();
   if ((tm == 2 || (tm == 1 && S == 1)) && (f.mode == 1 || (f.mode == 0 && f.fold_mod > 0))) {

@@ -18,12 +18,18 @@ ap.add_argument('a')
 ap.add_argument('b')
 ap.add_argument('--bf16', action='store_true')
 ap.add_argument('--wide', action='store_true', help='feature_sizes [32..512] (config-3 widths)')
+ap.add_argument('--env-a', default='', help='K=V[,K=V] for run a only (A/B of an environment switch)')
+ap.add_argument('--env-b', default='', help='K=V[,K=V] for run b only')
 args = ap.parse_args()
+
+
+def _kv(spec):
+    return dict(kv.split('=', 1) for kv in spec.split(',') if kv)
 kw = tm.KW.replace('[8, 16, 32, 64, 128]', '[32, 64, 128, 256, 512]') if args.wide else tm.KW
 env = {'HCU_TEST_BF16': '1' if args.bf16 else '0'}
 tmp = pathlib.Path(tempfile.mkdtemp())
-ra = tm._run(tmp, 'a', dict(env, HCU_LIB_PATH=args.a), kw=kw)
-rb = tm._run(tmp, 'b', dict(env, HCU_LIB_PATH=args.b), kw=kw)
+ra = tm._run(tmp, 'a', dict(env, HCU_LIB_PATH=args.a, **_kv(args.env_a)), kw=kw)
+rb = tm._run(tmp, 'b', dict(env, HCU_LIB_PATH=args.b, **_kv(args.env_b)), kw=kw)
 diff = [(it, k, (x.double() - y.double()).abs().max().item())
         for it in range(3) for k, (x, y) in enumerate(zip(ra[it], rb[it])) if not torch.equal(x, y)]
 print('bitwise equal' if not diff else 'DIFFERENT: %d tensors, first %s' % (len(diff), diff[:5]))
