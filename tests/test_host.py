@@ -195,3 +195,25 @@ def test_tiling_table_modes_and_file(tmp_path):
             _lib.tuning_mode(3)
     finally:
         _lib.tuning_mode(old)
+
+
+def test_bench_rocprof_names_map_to_timed_labels():
+    """bench.py reads the committed rocprofv3 summaries by the labels its
+    HIP-event timing uses (tagify): element-type templates, the bconv flags
+    and the 4-parameter bwgrad pipelines (equal A / G prefetch depths are
+    timed as <MSW,NS,NP>, the all-taps form keeps both), and every dominant
+    kernel a bench line names is found in this round's summaries."""
+    import bench
+    t = bench.tagify
+    assert t('void hcu::bconv_kernel<float, 4, 1, 1, 4, 0>(hcu::GConvArgs)') == 'bconv_kernel<f32,4,1,1,4>'
+    assert t('void hcu::bconv_kernel<unsigned short, 4, 2, 4, 12, 1>(hcu::GConvArgs)') == \
+        'bconv_kernel<bf16,4,2,4,12,bnb>'
+    assert t('void hcu::bwgrad_pipe_kernel<5, 4, 16, 16>(hcu::WGradArgs)') == 'bwgrad_pipe_kernel<5,4,16>'
+    assert t('void hcu::bwgrad_pipe_kernel<32, 1, 12, 8>(hcu::WGradArgs)') == 'bwgrad_pipe_kernel<32,1,12,8>'
+    assert t('void hcu::bn_bwd_apply_vec_kernel<float>(float*, float const*, hcu::BNCoef, long, int)') == \
+        'bn_bwd_apply_vec_kernel'
+    for cfg, kern in (('2', 'bconv_kernel<f32,4,1,1,4>'), ('3', 'bwgrad_pipe_kernel<5,4,16>')):
+        assert bench.rocprof_avg_us(kern, cfg) is not None, (cfg, kern)
+        assert bench.rocprof_avg_us(kern, cfg, 'serial_') is not None, (cfg, kern)
+        assert bench.load_traffic(kern, cfg) is not None, (cfg, kern)
+    assert bench.rocprof_avg_us('bconv_kernel<bf16,1,1,4,8>', 'runet') is not None
