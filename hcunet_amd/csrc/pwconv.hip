@@ -361,7 +361,7 @@ int pw_check(const void *const *parts, int nparts, int part_c, int part_cs, int6
   if (!parts || nparts < 1 || nparts > hcu::kPwMaxParts || part_c < 1 || part_cs % 8 || part_c > part_cs ||
       Cout < 1 || out_cs % 8 || Cout > out_cs || nvox < 0)
     return hcu::fail(1, std::string(who) + ": 1..8 parts of part_cs (a multiple of 8) slots, Cout <= out_cs");
-  for (int i = 0; i < nparts; ++i)
+  for (int i = 0; i < nparts && nvox > 0; ++i)   // (empty tensors may have null data)
     if (!parts[i] || reinterpret_cast<uintptr_t>(parts[i]) % 16)
       return hcu::fail(1, std::string(who) + ": parts must be non-null and 16-byte aligned");
   if (!hcu::pw_supported(nparts * part_cs, out_cs, Cout, false) ||
@@ -375,8 +375,8 @@ int pw_check(const void *const *parts, int nparts, int part_c, int part_cs, int6
 extern "C" int hcu_pw_conv_forward(const void *const *parts, int nparts, int part_c, int part_cs, const float *w,
                                    const float *b, void *out, int64_t nvox, int Cout, int out_cs, void *stream) {
   if (int e = pw_check(parts, nparts, part_c, part_cs, nvox, Cout, out_cs, "hcu_pw_conv_forward")) return e;
-  if (!w || !out) return hcu::fail(1, "hcu_pw_conv_forward: null weight or output");
   if (nvox == 0) return 0;
+  if (!w || !out) return hcu::fail(1, "hcu_pw_conv_forward: null weight or output");
   hcu::PwArgs a{};
   a.in = static_cast<const uint16_t *>(parts[0]);
   a.w = w;
@@ -404,7 +404,15 @@ extern "C" int hcu_pw_conv_backward(const void *const *parts, int nparts, int pa
                                     float *db, int64_t nvox, float *work, size_t work_floats, int accumulate,
                                     void *stream) {
   if (int e = pw_check(parts, nparts, part_c, part_cs, nvox, Cout, out_cs, "hcu_pw_conv_backward")) return e;
-  if (!w || !dout || !dw || !work) return hcu::fail(1, "hcu_pw_conv_backward: null weight, gradient or workspace");
+  if (!w || !dw) return hcu::fail(1, "hcu_pw_conv_backward: null weight or weight gradient");
+  if (nvox == 0) {   // no voxels: zero gradients (accumulate: nothing to add)
+    if (!accumulate) {
+      HCU_HIP(hipMemsetAsync(dw, 0, sizeof(float) * (size_t)Cout * nparts * part_c, (hipStream_t)stream));
+      if (db) HCU_HIP(hipMemsetAsync(db, 0, sizeof(float) * (size_t)Cout, (hipStream_t)stream));
+    }
+    return 0;
+  }
+  if (!dout || !work) return hcu::fail(1, "hcu_pw_conv_backward: null gradient or workspace");
   if (work_floats < hcu_pw_conv_work_floats(nvox, nparts, part_cs, Cout))
     return hcu::fail(1, "hcu_pw_conv_backward: workspace too small (hcu_pw_conv_work_floats)");
   hipStream_t s = (hipStream_t)stream;

@@ -532,3 +532,58 @@ def test_rdcnet_bf16_cat_free_mixing_matches_cat_and_chain(monkeypatch):
     assert torch.equal(o0, o1) and l0 == l1
     for (k, _), a, b in zip(net.named_parameters(), g0, g1):
         assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize('nparts,part_c,cout,nvox', [(5, 10, 10, 786), (2, 10, 10, 333), (1, 16, 16, 17),
+                                                      (3, 8, 5, 1), (2, 10, 10, 0)])
+def test_pw_conv_c_abi_matches_torch(nparts, part_c, cout, nvox):
+    """hcu_pw_conv_forward / _backward (include/hcunet.h) on their own: the
+    cat of `nparts` channels-last bf16 parts of part_c channels (16-byte
+    padded slots) through a 1x1x1 Conv3d, against fp64 torch on the same
+    bf16-representable operands -- ragged voxel counts (not a multiple of the
+    kernels' 16-voxel groups), a single voxel and an empty input; input
+    gradients in the parts' layout with their padding slots 0; dW / db
+    accumulated onto existing values (accumulate = 1)."""
+    import ctypes
+    from hcunet_amd import _lib
+    from hcunet_amd.chain import cl_channels
+    dev = torch.device('cuda', 0)
+    g = torch.Generator().manual_seed(nparts * 100 + nvox)
+    pcs, ocs = cl_channels(part_c, True), cl_channels(cout, True)
+    cin = nparts * part_c
+    w = torch.randn(cout, cin, generator=g).bfloat16().float()
+    b = torch.randn(cout, generator=g)
+    xs = [torch.randn(nvox, part_c, generator=g).bfloat16().float() for _ in range(nparts)]
+    dy = torch.randn(nvox, cout, generator=g).bfloat16().float()
+    x = torch.cat(xs, 1).double() if nvox else torch.zeros(0, cin, dtype=torch.float64)
+    y = x @ w.double().t() + b.double()
+    dx = dy.double() @ w.double()
+    dw = dy.double().t() @ x
+    db = dy.double().sum(0)
+    pad = lambda t, c: torch.nn.functional.pad(t, (0, c - t.shape[1])).to(torch.bfloat16).to(dev).contiguous()  # noqa: E731
+    parts = [pad(t, pcs) for t in xs]
+    out = torch.empty(nvox, ocs, dtype=torch.bfloat16, device=dev)
+    L = _lib.lib()
+    ptrs = (ctypes.c_void_p * nparts)(*[p.data_ptr() for p in parts])
+    wd, bd = w.to(dev), b.to(dev)
+    st = _lib.stream_handle(dev)
+    _lib.check(L.hcu_pw_conv_forward(ptrs, nparts, part_c, pcs, _lib.ptr(wd), _lib.ptr(bd), _lib.ptr(out),
+                                     nvox, cout, ocs, st), 'pw forward')
+    dparts = [torch.full_like(p, 7.0) for p in parts]
+    dptrs = (ctypes.c_void_p * nparts)(*[d.data_ptr() for d in dparts])
+    gw, gb = torch.ones(cout, cin, device=dev), torch.ones(cout, device=dev)   # accumulated onto
+    nw = int(L.hcu_pw_conv_work_floats(nvox, nparts, pcs, cout))
+    work = torch.empty(max(nw, 1), device=dev)
+    _lib.check(L.hcu_pw_conv_backward(ptrs, nparts, part_c, pcs, _lib.ptr(wd), _lib.ptr(pad(dy, ocs)), cout, ocs,
+                                      dptrs, _lib.ptr(gw), _lib.ptr(gb), nvox, _lib.ptr(work), nw, 1, st),
+               'pw backward')
+    torch.cuda.synchronize()
+    assert not out[:, cout:].any()
+    got_dx = torch.cat([d[:, :part_c] for d in dparts], 1).float().cpu() if nvox else torch.zeros(0, cin)
+    for d in dparts:
+        assert not d[:, part_c:].any()
+    scale = lambda t: max(t.abs().max().item() if t.numel() else 0.0, 1e-6)  # noqa: E731
+    assert (out[:, :cout].float().cpu().double() - y).abs().max().item() <= 1e-2 * scale(y) if nvox else True
+    assert (got_dx.double() - dx).abs().max().item() <= 1e-2 * scale(dx) if nvox else True
+    assert (gw.cpu().double() - 1 - dw).abs().max().item() <= 2e-3 * scale(dw) + 1e-6
+    assert (gb.cpu().double() - 1 - db).abs().max().item() <= 2e-3 * scale(db) + 1e-6
