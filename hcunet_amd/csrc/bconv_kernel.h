@@ -172,9 +172,11 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
   if (tid == 0) sa = a;
   const int T = a.KX * a.KY * a.KZ;
   const int S = (T + TPS - 1) / TPS;
-  const int HZ = a.HZ, HYZ = a.HY * a.HZ;
-  const int HV = a.HX * HYZ;
-  E *alds = reinterpret_cast<E *>(smem);                          // [HV][CKP] + a dummy slot
+  // halo image rows: (hx, hy, hz) at hx * hsx + hy * hsy + hz * hsz (the
+  // planner's axis order / padding), a dummy slot at row hvp
+  const int hsx = a.hsx, hsy = a.hsy, hsz = a.hsz;
+  const int HV = a.HX * a.HY * a.HZ, HVP = a.hvp;
+  E *alds = reinterpret_cast<E *>(smem);                          // [hvp][CKP] + a dummy slot
   E *wlds = reinterpret_cast<E *>(smem + a.areg);                 // [S][4][NT][VEC]
   int *toffs = reinterpret_cast<int *>(wlds + S * 4 * NT * VEC);  // [S][4]
   int *rowpk = toffs + S * 4;                                     // [MPW*64]
@@ -204,7 +206,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
       int q, lz, lx, ly;
       a.fTZ.divmod(i, q, lz);
       a.fTY.divmod(q, lx, ly);
-      v = lx * a.sx * HYZ + ly * a.sy * HZ + lz * a.sz;
+      v = lx * a.sx * hsx + ly * a.sy * hsy + lz * a.sz * hsz;
     }
     vb[j] = v * CKP;
   }
@@ -225,7 +227,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     int off = 0;
     if (t < T) {
       const int kz = t % a.KZ, q = t / a.KZ, ky = q % a.KY, kx = q / a.KY;
-      off = kx * a.dx * HYZ + ky * a.dy * HZ + kz * a.dz;
+      off = kx * a.dx * hsx + ky * a.dy * hsy + kz * a.dz * hsz;
     }
     toffs[e] = off * CKP + ((e & 3) % CV) * VEC;
   }
@@ -504,6 +506,7 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
     for (int base = tid / CV; base < HV; base += 4 * VS) {
       uint4 val[4];
       bool okv[4];
+      int hrow[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int v = base + u * VS;
@@ -517,12 +520,13 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
                            : 0x7ffffff0;
         val[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
         okv[u] = ok;
+        hrow[u] = hx * hsx + hy * hsy + hz * hsz;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int v = base + u * VS;
         if (v < HV)
-          *reinterpret_cast<uint4 *>(alds + v * CKP + cv * VEC) =
+          *reinterpret_cast<uint4 *>(alds + hrow[u] * CKP + cv * VEC) =
               activate(val[u], okv[u], chunk);
       }
     }
@@ -557,8 +561,8 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
         w = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
       }
       const int hp = hpk[u];
-      *reinterpret_cast<uint4 *>(alds + (hp >= 0 ? (tid + u * VS) * CKP : HV * CKP)) = w;
       const int hx = hp >> 20, hy = (hp >> 10) & 1023, hz = hp & 1023;
+      *reinterpret_cast<uint4 *>(alds + (hp >= 0 ? (hx * hsx + hy * hsy + hz * hsz) * CKP : HVP * CKP)) = w;
       if (xo && ok && (hx < KA(TX) || lastx) && (hy < KA(TY) || lasty) && (hz < KA(TZ) || lastz)) {
         const size_t vox = (((size_t)b * IX + ox0 * KA(sx) - KA(px) + hx) * IY + oy0 * KA(sy) - KA(py) + hy) * IZ +
                            oz0 * KA(sz) - KA(pz) + hz;
@@ -756,9 +760,12 @@ __global__ void __launch_bounds__(256) bconv_kernel(const GConvArgs a) {
           ncx_store(b, ox0, oy0, oz0);
         } else {
 #pragma unroll
-        for (int u = 0; u < NPFR; ++u)   // every element is written (the waits stay exact)
-          *reinterpret_cast<uint4 *>(alds + (hpk[u] >= 0 ? (tid / CV + u * VS) * CKP + cv * VEC : HV * CKP)) =
+        for (int u = 0; u < NPFR; ++u) {   // every element is written (the waits stay exact)
+          const int hp = hpk[u];
+          const int row = (hp >> 20) * hsx + ((hp >> 10) & 1023) * hsy + (hp & 1023) * hsz;
+          *reinterpret_cast<uint4 *>(alds + (hp >= 0 ? row * CKP + cv * VEC : HVP * CKP)) =
               activate(pf[u], (okbits >> u) & 1u, chunk);
+        }
         }
         PH_MARK(0);
         if (wpre)

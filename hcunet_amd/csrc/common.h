@@ -218,6 +218,10 @@ struct GConvArgs {
   // tiling (filled by plan_gconv)
   int TX, TY, TZ, ntx, nty, ntz;
   int HX, HY, HZ, P;
+  // bconv halo image in LDS: row strides of the x / y / z halo axes and the
+  // row count they span (plan-chosen axis order and padding; default
+  // HY*HZ, HZ, 1 and HX*HY*HZ)
+  int hsx, hsy, hsz, hvp;
   int CK, NSUB, MPW;
   int lds_bytes;
   FastDiv fHZ, fHY, fTZ, fTY;         // halo / tile index decomposition
