@@ -447,14 +447,15 @@ static double halo_read_cycles(const GConvArgs &a, int CV, int px, int py, int p
 // A-fragment reads take the fewest LDS cycles, within the LDS cap.  The layout
 // only moves where a halo element sits in LDS: every product and sum is the
 // same (bitwise-equal results).  HCU_HALO_LAYOUT=0 keeps the dense z-fastest
-// image.
+// image; =2 searches the fp32 tiles too (measured neutral on configs 2/3:
+// their 16x16x4 fp32 MFMA, not LDS, bounds those tiles).
 static void bconv_halo_layout(GConvArgs &a, int CV, long lds_cap) {
   a.hsx = a.HY * a.HZ;
   a.hsy = a.HZ;
   a.hsz = 1;
   a.hvp = a.HX * a.HY * a.HZ;
   static const int on = env_int_b("HCU_HALO_LAYOUT", 1);
-  if (a.bes != 2 || !on) return;
+  if (!on || (a.bes != 2 && on < 2)) return;
   const int NT = a.NSUB * 16;
   const int dim[3] = {a.HX, a.HY, a.HZ};
   static const int orders[6][3] = {{2, 1, 0}, {2, 0, 1}, {1, 2, 0}, {1, 0, 2}, {0, 2, 1}, {0, 1, 2}};
