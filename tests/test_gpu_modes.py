@@ -104,6 +104,20 @@ def test_bf16_steps_are_deterministic(tmp_path):
     assert not bad, bad[:8]
 
 
+@pytest.mark.parametrize('bf16', ['0', '1'])
+def test_halo_layout_is_bitwise_neutral(tmp_path, bf16):
+    """bconv's planner-chosen halo image layout in LDS (axis order and row
+    padding, bconv.hip bconv_halo_layout) only moves where each halo element
+    sits: outputs and gradients over 3 training steps are bitwise equal to the
+    dense z-fastest image (HCU_HALO_LAYOUT=0).  fp32 runs the search with
+    HCU_HALO_LAYOUT=2 (off by default there)."""
+    kw = KW if bf16 == '0' else KW.replace('[8, 16, 32, 64, 128]', '[16, 32, 64, 128]')
+    dense = _run(tmp_path, 'hl0' + bf16, {'HCU_HALO_LAYOUT': '0', 'HCU_TEST_BF16': bf16}, kw=kw)
+    laid = _run(tmp_path, 'hl2' + bf16, {'HCU_HALO_LAYOUT': '2', 'HCU_TEST_BF16': bf16}, kw=kw)
+    bad = [(it, k) for it in range(3) for k, (x, y) in enumerate(zip(dense[it], laid[it])) if not torch.equal(x, y)]
+    assert not bad, bad[:8]
+
+
 def test_fresh_input_every_step_matches():
     """A new input tensor each step (data-loader pattern: the input layout change
     runs ahead of the captured graph) gives the same outputs and gradients as
